@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark: vectors quantized/sec of the 3-level RQ encode (512-d, [128,128,256]) on MI355X.
+
+Workload (BASELINE.json configs[2], the largest single-GPU config): 10M x 512 fp32
+synthetic song vectors per GPU (Gaussian mixture, generated on the device), PROD
+codebooks (layer_clusters [128,1280,1280], need [128,128,256]: C1 128 x 512,
+C2 16384 x 512, C3 2560 x 512 + a 16384 x 2560 match matrix with 256 allowed
+columns per (l1,l2) group), training-consistent encode semantics (exact argmin,
+normalised residuals).  A step = one full 3-level encode of the rank's batch,
+inputs resident in HBM.  Multi-GPU: one process per GPU, rows sharded (weak
+scaling: every rank encodes its own 10M rows), no data-path collective; the
+timed region is bracketed by barrier + synchronize and the max over ranks is
+taken.
+
+Extra fields: ``roofline`` for the dominant kernel (per-launch time from HIP
+events on the launch stream inside the timed region), ``kernels`` (per-level
+breakdown), ``cpu_baseline`` (the oracle's CPU encode timed on this host on a
+bounded sample, rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+
+from generative_ranking_recommender_amd import ops, synth  # noqa: E402
+from generative_ranking_recommender_amd.encode import HIERARCHICAL_TRAIN, RQEncoder  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA spec
+D = 512
+NEED = [128, 128, 256]
+N_CAND = 2560
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rows", type=int, default=10_000_000, help="rows per GPU")
+    ap.add_argument("--cpu-sample", type=int, default=200_000, help="rows for the CPU baseline (0 = skip)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+class Timed:
+    """HIP-event brackets recorded on torch's current stream (the stream every rqsid call uses)."""
+
+    def __init__(self):
+        self.pairs = {}
+
+    def wrap(self, name, fn):
+        def inner(*a, **k):
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            out = fn(*a, **k)
+            e.record()
+            self.pairs.setdefault(name, []).append((s, e))
+            return out
+        return inner
+
+    def mean_ms(self):
+        return {k: float(np.mean([s.elapsed_time(e) for s, e in v])) for k, v in self.pairs.items()}
+
+
+def make_rows(n, rank, device):
+    g = torch.Generator(device=device).manual_seed(1234 + rank)
+    means = torch.from_numpy(synth.blob_means()).to(device)
+    x = torch.empty((n, D), dtype=torch.float32, device=device)
+    step = 1 << 20
+    for i in range(0, n, step):
+        m = min(step, n - i)
+        lab = torch.randint(0, means.shape[0], (m,), device=device, generator=g)
+        x[i:i + m] = means[lab] + 0.25 * torch.randn((m, D), device=device, generator=g)
+    return x
+
+
+def cpu_baseline(cb, rows):
+    from threadpoolctl import threadpool_info
+    from oracle import rq_oracle as O
+    x = synth.mixture_rows(0, rows)
+    t = time.perf_counter()
+    O.encode(x, [cb["c0"], cb["c1"], cb["c2"]], NEED, cb["match"], residual_from_weighted=True)
+    dt = time.perf_counter() - t
+    threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    return {"value": rows / dt, "unit": "vectors/s", "cores": int(threads), "kind": "port",
+            "sample": f"{rows} rows x 3 levels, oracle/rq_oracle.py encode (numpy fp32 BLAS, {threads} threads), "
+                      f"{dt:.2f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    cb = synth.encode_codebooks(seed=99)
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], NEED, match=torch.from_numpy(cb["match"]),
+                    semantics=HIERARCHICAL_TRAIN, device=dev)
+    n = args.rows
+    x = make_rows(n, rank, dev)
+    torch.cuda.synchronize()
+
+    # instrument the kernels (events only; no host sync inside the timed region)
+    timer = Timed()
+    orig_assign, orig_res, orig_bucket = ops.assign, ops.residual, ops.bucket
+    level = {"i": 0}
+
+    def assign_hook(*a, **k):
+        name = f"assign_l{level['i']}"
+        level["i"] += 1
+        return timer.wrap(name, orig_assign)(*a, **k)
+
+    import generative_ranking_recommender_amd.encode as encmod
+
+    for _ in range(args.warmup):
+        enc.encode(x)
+    torch.cuda.synchronize()
+    rescored = []
+    enc.encode(x, count_rescored=True)
+    rescored = list(enc.last_rescored)
+
+    encmod.ops.assign = assign_hook
+    encmod.ops.residual = timer.wrap("residual", orig_res)
+    encmod.ops.bucket = timer.wrap("bucket", orig_bucket)
+
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        level["i"] = 0
+        out = enc.encode(x)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    encmod.ops.assign, encmod.ops.residual, encmod.ops.bucket = orig_assign, orig_res, orig_bucket
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist:
+        tdist.all_reduce(el, op=tdist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    ms = timer.mean_ms()
+
+    # roofline of the dominant kernel (algorithmic bytes / flops per launch)
+    bytes_row = D * 4 + 4
+    kern = {}
+    for lvl, keff in ((0, NEED[0]), (1, NEED[1]), (2, NEED[2])):
+        t = ms.get(f"assign_l{lvl}")
+        if t is None:
+            continue
+        gbs = n * bytes_row / (t * 1e-3) / 1e9
+        tfl = n * 2 * keff * D / (t * 1e-3) / 1e12
+        kern[f"assign_l{lvl}"] = {"ms": round(t, 3), "GB/s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                                  "fp32_equiv_TFLOP/s": round(tfl, 1),
+                                  "bf16x3_mfma_frac": round(3 * tfl / BF16_PEAK_TFLOPS, 4),
+                                  "rescored_rows": rescored[lvl] if lvl < len(rescored) else None}
+    if "residual" in ms:
+        t = ms["residual"]
+        gbs = n * (3 * D * 4) / (t * 1e-3) / 1e9
+        kern["residual"] = {"ms": round(t, 3), "GB/s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+    if "bucket" in ms:
+        kern["bucket"] = {"ms": round(ms["bucket"], 3)}
+    dom = max((k for k in kern if k.startswith("assign")), key=lambda k: kern[k]["ms"])
+    dk = kern[dom]
+    roof = {"kernel": dom + " (rqsid_assign: assign_screen_kernel + fp64 re-score)", "bound": "hbm",
+            "achieved": dk["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dk["hbm_frac"],
+            "traffic": None, "bytes_per_row": bytes_row}
+
+    total_rows = n * world * args.steps
+    value = total_rows / elapsed
+    line = {
+        "metric": "vectors quantized/sec (3-level RQ, 512-d)",
+        "value": round(value, 1),
+        "unit": "vectors/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic Gaussian mixture (4096 blobs, sigma 0.25) generated on device; synthetic residual codebooks",
+        "config": {"workload": f"3-level RQ encode, {n} x {D} fp32 rows per GPU, need [128,128,256], "
+                               "layer_clusters [128,1280,1280] (BASELINE configs[2]/[3])",
+                   "rows_per_gpu": n, "dim": D, "need_clusters": NEED, "candidates_last_level": N_CAND,
+                   "parallelism": f"rows sharded x{world}, no collective",
+                   "method": "bf16x3 MFMA screen + fp64 re-score (exact argmin)"},
+        "roofline": roof,
+        "kernels": kern,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
+        line["cpu_baseline"] = cpu_baseline(cb, args.cpu_sample)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,87 @@
+"""Loader for the in-tree HIP library ``librqsid.so`` (C ABI: ``include/rqsid.h``).
+
+The product path has no CPU fallback: if the library is missing or no GPU is
+visible the calls below raise.  ``build()`` compiles ``csrc/rqsid.hip`` for
+gfx950 with hipcc into the package directory, so the ``.so`` travels with the
+repository snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+REPO = PKG.parent
+LIB_PATH = PKG / "librqsid.so"
+SRC = PKG / "csrc" / "rqsid.hip"
+HEADER = REPO / "include" / "rqsid.h"
+
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC"]
+
+c_i32, c_i64, c_f32, c_vp, c_char_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_char_p
+
+# name -> (restype, argtypes); mirrors include/rqsid.h one to one
+SIGNATURES = {
+    "rqsid_version": (c_i32, []),
+    "rqsid_last_error": (c_char_p, []),
+    "rqsid_prepare_centers": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "rqsid_bucket_workspace_bytes": (c_i64, [c_i64, c_i32]),
+    "rqsid_bucket": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "rqsid_assign_tile_rows": (c_i32, []),
+    "rqsid_assign_workspace_bytes": (c_i64, [c_i64]),
+    "rqsid_assign": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_i64,
+                             c_vp, c_vp, c_vp, c_vp, c_i32,
+                             c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "rqsid_residual": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
+    "rqsid_scale_groups": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp]),
+    "rqsid_centroid_tile_rows": (c_i32, []),
+    "rqsid_centroid_accumulate": (c_i32, [c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "rqsid_centroid_finalize": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
+    "rqsid_match_workspace_bytes": (c_i64, [c_i32]),
+    "rqsid_match_to_candidates": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "rqsid_pairwise_distance": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp]),
+}
+
+_lib = None
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile the HIP library for gfx950 (hipcc cross-compiles without a GPU)."""
+    if LIB_PATH.exists() and not force and LIB_PATH.stat().st_mtime >= max(SRC.stat().st_mtime, HEADER.stat().st_mtime):
+        return LIB_PATH
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [hipcc, *HIPCC_FLAGS, "-o", str(tmp), str(SRC)]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def load():
+    """Load librqsid.so and bind every symbol of include/rqsid.h (raises if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(
+            f"HIP library {LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback for the semantic-ID kernels)")
+    lib = ctypes.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().rqsid_last_error().decode(errors="replace")
+        if rc == -1:
+            raise ValueError(f"{what}: {msg}")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")

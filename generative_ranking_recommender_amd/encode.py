@@ -1,0 +1,147 @@
+"""Multi-level residual-quantisation encoder on the HIP kernels (the bench hot path).
+
+One ``RQEncoder`` holds the trained codebooks of every level, already prepared
+for ``rqsid_assign`` (bf16 split, norms, candidate lists), and turns an fp32
+[N, D] device matrix into int32 [N, L] semantic IDs with no host round trip.
+
+Level semantics:
+
+* level 0: nearest of ``need[0]`` centres (``_predict_layer_0``,
+  hierarchical_rq_kmeans.py:1146-1173; simplified :202).
+* middle level l: segment = the previous level's ID p; allowed centres are the
+  block ``[p*need[l], (p+1)*need[l])``; the ID is the local index in the block
+  (``_predict_middle_layer`` :1175-1233 / ``_reassign_clusters_middle_layer_with_
+  residuals`` :839-904 / simplified :145-172).
+* last level: group = ``ids[l-2]*mult + ids[l-1]`` (mult = ``need[l-2]`` in the
+  hierarchical path :824,1256, ``need[-2]`` in the simplified path :311); allowed
+  centres = the group's match-matrix row.  ID = rank of the chosen column among
+  the allowed ones (``_merge_match_matrix_cluster_ids`` :1055-1086) or the raw
+  column (simplified :305-331).
+
+Switches reproduce the reference's predict-time quirks (Appendix A item 2):
+``match_lookup`` False = the `match_matrices[layer-1]` miss at :1248 (the last
+level is then an unconstrained argmin over every candidate, raw IDs);
+``residual_global_id`` False = predict's residual indexing ``centers[id % need]``
+(:577,1143) instead of the raw block index the trainer uses (:901).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import ops
+
+
+@dataclass
+class LevelSemantics:
+    normalize_residual: bool = True      # hierarchical: r/(||r||+1e-8) per group; simplified: plain
+    match_lookup: bool = True            # False: reference predict bug (:1248)
+    residual_global_id: bool = True      # False: reference predict bug (:1143 with modded ids)
+    remap_last: bool = True              # hierarchical rank remap; simplified keeps raw column
+    last_group_mult: str = "need_l_minus_2"  # or "need_minus_2" (simplified)
+    residual_from_weighted: bool = False  # train-time residuals use weighted data (:442 vs :577)
+
+
+HIERARCHICAL_PREDICT_REFERENCE = LevelSemantics(match_lookup=False, residual_global_id=False)
+HIERARCHICAL_TRAIN = LevelSemantics(residual_from_weighted=True)
+SIMPLIFIED = LevelSemantics(normalize_residual=False, remap_last=False, last_group_mult="need_minus_2")
+
+
+class RQEncoder:
+    def __init__(self, centers: Sequence[torch.Tensor], need_clusters: Sequence[int],
+                 match: Optional[torch.Tensor] = None, group_dims: Sequence[int] = (),
+                 weights: Optional[Sequence[Sequence[float]]] = None,
+                 semantics: LevelSemantics = LevelSemantics(), device=None):
+        device = device or torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        self.L = len(centers)
+        self.need = list(need_clusters)
+        self.sem = semantics
+        self.dim = centers[0].shape[1]
+        self.group_dims = list(group_dims) or [self.dim]
+        self.weights = None
+        if weights is not None and any(any(w != 1.0 for w in ws) for ws in weights):
+            self.weights = [list(ws) for ws in weights]
+        self.pcs = [ops.prepare_centers(c.to(device)) for c in centers]
+        self.cands: List[Optional[ops.Candidates]] = []
+        self.has_penalty = False
+        for l in range(self.L):
+            if l == 0:
+                self.cands.append(ops.Candidates(torch.zeros(1, dtype=torch.int32, device=device),
+                                                 torch.full((1,), self.pcs[0].k, dtype=torch.int32, device=device),
+                                                 self.pcs[0].k))
+            elif l < self.L - 1:
+                self.cands.append(ops.contiguous_candidates(self.need[l - 1], self.need[l], device))
+            else:
+                if match is not None and semantics.match_lookup:
+                    m = match.to(device)
+                    c = ops.match_to_candidates(m)
+                    self.has_penalty = bool((c.count == 0).any().item())
+                    self.n_groups = m.shape[0]
+                    self.cands.append(c)
+                else:
+                    k = self.pcs[l].k
+                    self.cands.append(ops.Candidates(torch.zeros(1, dtype=torch.int32, device=device),
+                                                     torch.full((1,), k, dtype=torch.int32, device=device), k))
+        self._ws = None
+        self.last_rescored = []
+
+    def _workspace(self, n):
+        if self._ws is None or self._ws.n_rows < n:
+            self._ws = ops.AssignWorkspace(n, self.device)
+        return self._ws
+
+    def _weighted(self, x, l):
+        if self.weights is None:
+            return x
+        return ops.scale_groups(x, self.group_dims, self.weights[l])
+
+    def encode(self, x: torch.Tensor, count_rescored: bool = False) -> torch.Tensor:
+        """x: f32 [N, D] on the device -> int32 [N, L] semantic IDs."""
+        if x.dim() != 2 or x.shape[1] != self.dim:
+            raise ValueError(f"Input dimension {x.shape[-1]} does not match config embedding_dim {self.dim}")
+        x = x.float().contiguous()
+        n = x.shape[0]
+        out = torch.empty((self.L, n), dtype=torch.int32, device=x.device)
+        ws = self._workspace(n)
+        cur = x
+        self.last_rescored = []
+        if self.L == 2:
+            raise IndexError("list index out of range")  # reference: all_cluster_ids[-2] with one level
+        glob = torch.empty(n, dtype=torch.int32, device=x.device)
+        for l in range(self.L):
+            w = self._weighted(cur, l)
+            if l == 0:
+                b = ops.single_segment(n, x.device)
+                ops.assign(w, self.pcs[0], b, self.cands[0], out_local=out[0], out_global=glob, workspace=ws)
+                out[0].copy_(glob)
+            elif l < self.L - 1:
+                b = ops.bucket(out[l - 1], self.need[l - 1])
+                ops.assign(w, self.pcs[l], b, self.cands[l], out_local=out[l], out_global=glob, workspace=ws)
+            else:
+                if self.sem.match_lookup:
+                    mult = self.need[l - 2] if self.sem.last_group_mult == "need_l_minus_2" else self.need[-2]
+                    grp = out[l - 2] * mult + out[l - 1]
+                    if mult < self.need[l - 1] and int(grp.max().item()) >= self.n_groups:
+                        raise IndexError(f"index {int(grp.max().item())} is out of bounds for axis 0 with size "
+                                         f"{self.n_groups}")
+                    b = ops.bucket(grp, self.n_groups)
+                else:
+                    b = ops.single_segment(n, x.device)
+                ops.assign(w, self.pcs[l], b, self.cands[l], out_local=out[l], out_global=glob, workspace=ws)
+                if not (self.sem.match_lookup and self.sem.remap_last):
+                    out[l].copy_(glob)
+                elif self.has_penalty:
+                    bad = torch.nonzero(out[l] < 0)
+                    if bad.numel():
+                        # reference: mapping_result[prev_id][cur_id] KeyError (:1084)
+                        raise KeyError(int(glob[bad[0, 0]].item()))
+            if count_rescored:
+                self.last_rescored.append(ws.rescored())
+            if l < self.L - 1:
+                src = w if self.sem.residual_from_weighted else cur
+                cid = glob if self.sem.residual_global_id else out[l]
+                cur = ops.residual(src, self.pcs[l].centers, cid, self.group_dims, self.sem.normalize_residual)
+        return out.t().contiguous()

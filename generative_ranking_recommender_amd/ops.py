@@ -1,0 +1,239 @@
+"""Tensor-level wrappers over the C ABI (include/rqsid.h).
+
+Every function takes/returns DEVICE tensors on the current HIP device and
+enqueues on torch's current stream; nothing here synchronises with the host.
+There is deliberately no CPU implementation: a CPU tensor or a missing
+``librqsid.so`` raises.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+
+_ALIGN = 256
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _require_device(*ts: Optional[torch.Tensor]) -> None:
+    for t in ts:
+        if t is not None and t.device.type != "cuda":
+            raise RuntimeError("rqsid kernels run on the GPU only: got a %s tensor" % t.device.type)
+        if t is not None and not t.is_contiguous():
+            raise ValueError("rqsid kernels need contiguous tensors")
+
+
+def lib():
+    return _lib.load()
+
+
+def tile_rows() -> int:
+    return int(lib().rqsid_assign_tile_rows())
+
+
+def centroid_tile_rows() -> int:
+    return int(lib().rqsid_centroid_tile_rows())
+
+
+@dataclass
+class PreparedCenters:
+    """Centres + the derived data rqsid_assign reads (bf16 hi/lo split, |c|^2, |c|)."""
+    centers: torch.Tensor      # f32 [K, D]
+    split: torch.Tensor        # int16 [K, D/32, 64] (bf16 bits, hi chunk then lo chunk)
+    sqnorm: torch.Tensor       # f32 [K]
+    norm: torch.Tensor         # f32 [K]
+
+    @property
+    def k(self) -> int:
+        return self.centers.shape[0]
+
+
+def prepare_centers(c: torch.Tensor) -> PreparedCenters:
+    c = c.float().contiguous()
+    _require_device(c)
+    k, d = c.shape
+    split = torch.empty((k, d // 32, 64), dtype=torch.int16, device=c.device)
+    sq = torch.empty(k, dtype=torch.float32, device=c.device)
+    nrm = torch.empty(k, dtype=torch.float32, device=c.device)
+    _lib.check(lib().rqsid_prepare_centers(_ptr(c), k, d, _ptr(split), _ptr(sq), _ptr(nrm), _stream()),
+               "rqsid_prepare_centers")
+    return PreparedCenters(c, split, sq, nrm)
+
+
+@dataclass
+class Buckets:
+    """Rows grouped by segment key (counting sort), as consumed by rqsid_assign."""
+    seg_row_off: torch.Tensor   # i32 [S+1]
+    seg_tile_off: torch.Tensor  # i32 [S+1]
+    row_index: Optional[torch.Tensor]  # i32 [N] or None (identity)
+    n_segments: int
+    max_tiles: int
+
+
+def single_segment(n: int, device, rows_per_tile: Optional[int] = None) -> Buckets:
+    """All n rows in one segment, identity order (layer 0 / dense prediction)."""
+    tr = rows_per_tile or tile_rows()
+    off = torch.tensor([0, n], dtype=torch.int32, device=device)
+    toff = torch.tensor([0, (n + tr - 1) // tr], dtype=torch.int32, device=device)
+    return Buckets(off, toff, None, 1, (n + tr - 1) // tr)
+
+
+def bucket(keys: torch.Tensor, n_segments: int, rows_per_tile: Optional[int] = None) -> Buckets:
+    keys = keys.to(torch.int32).contiguous()
+    _require_device(keys)
+    n = keys.numel()
+    tr = rows_per_tile or tile_rows()
+    off = torch.empty(n_segments + 1, dtype=torch.int32, device=keys.device)
+    toff = torch.empty(n_segments + 1, dtype=torch.int32, device=keys.device)
+    idx = torch.empty(max(n, 1), dtype=torch.int32, device=keys.device)
+    wsb = int(lib().rqsid_bucket_workspace_bytes(n, n_segments))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=keys.device)
+    _lib.check(lib().rqsid_bucket(_ptr(keys), n, n_segments, tr, _ptr(off), _ptr(toff), _ptr(idx), _ptr(ws), wsb,
+                                  _stream()), "rqsid_bucket")
+    return Buckets(off, toff, idx[:n], n_segments, (n + tr - 1) // tr + n_segments)
+
+
+@dataclass
+class Candidates:
+    """Per-segment allowed centres: global index of local j = idx[base[s]+j] (idx None: base[s]+j)."""
+    base: torch.Tensor          # i32 [S]
+    count: torch.Tensor         # i32 [S]
+    count_max: int
+    idx: Optional[torch.Tensor] = None   # i32
+    flags: Optional[torch.Tensor] = None  # u8 [S]
+
+
+def contiguous_candidates(n_segments: int, per_segment: int, device) -> Candidates:
+    base = torch.arange(n_segments, dtype=torch.int32, device=device) * per_segment
+    cnt = torch.full((n_segments,), per_segment, dtype=torch.int32, device=device)
+    return Candidates(base, cnt, per_segment)
+
+
+def match_to_candidates(match: torch.Tensor) -> Candidates:
+    """uint8 [groups, n_cand] match matrix -> ascending allowed-column lists (+ penalty flags)."""
+    match = match.to(torch.uint8).contiguous()
+    _require_device(match)
+    g, nc = match.shape
+    base = torch.empty(g, dtype=torch.int32, device=match.device)
+    cnt = torch.empty(g, dtype=torch.int32, device=match.device)
+    flags = torch.empty(g, dtype=torch.uint8, device=match.device)
+    idx = torch.empty(g * nc, dtype=torch.int32, device=match.device)
+    wsb = int(lib().rqsid_match_workspace_bytes(g))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=match.device)
+    _lib.check(lib().rqsid_match_to_candidates(_ptr(match), g, nc, _ptr(base), _ptr(cnt), _ptr(idx), _ptr(flags),
+                                               _ptr(ws), wsb, _stream()), "rqsid_match_to_candidates")
+    # the maximum allowed count decides the kernel variant; match rows are host-known data
+    cmax = int(match.sum(1).max().item()) if g else 0
+    return Candidates(base, cnt, cmax, idx, flags)
+
+
+class AssignWorkspace:
+    """Re-usable scratch for rqsid_assign (rows needing an fp64 re-score)."""
+
+    def __init__(self, n_rows: int, device):
+        self.bytes = int(lib().rqsid_assign_workspace_bytes(n_rows))
+        self.buf = torch.empty(self.bytes, dtype=torch.uint8, device=device)
+        self.n_rows = n_rows
+
+    def rescored(self) -> int:
+        """Rows re-scored in fp64 by the last assign (host sync)."""
+        return int(self.buf[:4].view(torch.int32).item())
+
+
+def assign(x: torch.Tensor, pc: PreparedCenters, buckets: Buckets, cand: Candidates,
+           out_local: Optional[torch.Tensor] = None, out_global: Optional[torch.Tensor] = None,
+           workspace: Optional[AssignWorkspace] = None):
+    """Exact segmented argmin. Returns (local i32[N], global i32[N])."""
+    _require_device(x, pc.centers, cand.base, cand.count, cand.idx, cand.flags)
+    n, d = x.shape
+    if d != pc.centers.shape[1]:
+        raise ValueError(f"dimension mismatch: x has {d}, centres {pc.centers.shape[1]}")
+    dev = x.device
+    if out_local is None:
+        out_local = torch.empty(n, dtype=torch.int32, device=dev)
+    if out_global is None:
+        out_global = torch.empty(n, dtype=torch.int32, device=dev)
+    if workspace is None or workspace.n_rows < n:
+        workspace = AssignWorkspace(n, dev)
+    _lib.check(lib().rqsid_assign(
+        _ptr(x), n, d, _ptr(buckets.row_index), buckets.n_segments, _ptr(buckets.seg_row_off),
+        _ptr(buckets.seg_tile_off), buckets.max_tiles,
+        _ptr(pc.centers), _ptr(pc.split), _ptr(pc.sqnorm), _ptr(pc.norm), pc.k,
+        _ptr(cand.base), _ptr(cand.count), cand.count_max, _ptr(cand.idx), _ptr(cand.flags),
+        _ptr(out_local), _ptr(out_global), _ptr(workspace.buf), workspace.bytes, _stream()), "rqsid_assign")
+    return out_local, out_global
+
+
+def nearest(x: torch.Tensor, pc: PreparedCenters, workspace: Optional[AssignWorkspace] = None) -> torch.Tensor:
+    """Unconstrained nearest centre (KMeans.predict / pairwise_distance_full + argmin)."""
+    n = x.shape[0]
+    b = single_segment(n, x.device)
+    cand = Candidates(torch.zeros(1, dtype=torch.int32, device=x.device),
+                      torch.full((1,), pc.k, dtype=torch.int32, device=x.device), pc.k)
+    return assign(x, pc, b, cand, workspace=workspace)[1]
+
+
+def _groups_tensor(group_dims: Sequence[int], device) -> torch.Tensor:
+    return torch.tensor(list(group_dims), dtype=torch.int32, device=device)
+
+
+def residual(x: torch.Tensor, centers: torch.Tensor, ids: torch.Tensor, group_dims: Sequence[int] = (),
+             normalize: bool = True, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    ids = ids.to(torch.int32).contiguous()
+    centers = centers.float().contiguous()
+    _require_device(x, centers, ids)
+    n, d = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    gd = list(group_dims) or [d]
+    g = _groups_tensor(gd, x.device)
+    _lib.check(lib().rqsid_residual(_ptr(x), n, d, _ptr(centers), centers.shape[0], _ptr(ids), _ptr(g), len(gd), int(normalize),
+                                    _ptr(out), _stream()), "rqsid_residual")
+    return out
+
+
+def scale_groups(x: torch.Tensor, group_dims: Sequence[int], weights: Sequence[float]) -> torch.Tensor:
+    _require_device(x)
+    n, d = x.shape
+    out = torch.empty_like(x)
+    g = _groups_tensor(group_dims, x.device)
+    w = torch.tensor(list(weights), dtype=torch.float32, device=x.device)
+    _lib.check(lib().rqsid_scale_groups(_ptr(x), n, d, _ptr(g), len(group_dims), _ptr(w), _ptr(out), _stream()),
+               "rqsid_scale_groups")
+    return out
+
+
+def centroid_update(x: torch.Tensor, assignment: torch.Tensor, k: int, centers: torch.Tensor):
+    """New centres = per-cluster means of x (fp64 sums) written into ``centers`` where the
+    cluster is non-empty.  Returns (centers, counts i32[k])."""
+    _require_device(x, centers)
+    n, d = x.shape
+    b = bucket(assignment, k, rows_per_tile=centroid_tile_rows())
+    sums = torch.zeros((k, d), dtype=torch.float64, device=x.device)
+    _lib.check(lib().rqsid_centroid_accumulate(_ptr(x), d, _ptr(b.row_index), k, _ptr(b.seg_row_off),
+                                               _ptr(b.seg_tile_off), b.max_tiles, _ptr(sums), _stream()),
+               "rqsid_centroid_accumulate")
+    _lib.check(lib().rqsid_centroid_finalize(_ptr(sums), _ptr(b.seg_row_off), k, d, _ptr(centers), _stream()),
+               "rqsid_centroid_finalize")
+    counts = b.seg_row_off[1:] - b.seg_row_off[:-1]
+    return centers, counts
+
+
+def pairwise_distance(x: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
+    c = c.float().contiguous()
+    _require_device(x, c)
+    n, d = x.shape
+    out = torch.empty((n, c.shape[0]), dtype=torch.float32, device=x.device)
+    _lib.check(lib().rqsid_pairwise_distance(_ptr(x), n, d, _ptr(c), c.shape[0], _ptr(out), _stream()),
+               "rqsid_pairwise_distance")
+    return out

@@ -1,0 +1,138 @@
+/*
+ * rqsid.h — C ABI of the MI355X (gfx950) residual-quantisation semantic-ID kernels.
+ *
+ * The reference (zeehu/generative_ranking_recommender) has no FFI: its hot path
+ * is the Python module API of balancekmeans / hierarchical_rq_kmeans /
+ * simplified_semantic_id_generator, whose arithmetic is stock PyTorch ops.
+ * Each entry point below replaces one of those op sequences; the reference
+ * file:line it stands in for is cited per function.  The Python mirror of the
+ * reference classes (generative_ranking_recommender_amd/) binds these with
+ * ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - every pointer is a DEVICE pointer owned by the caller (e.g. torch
+ *    tensor.data_ptr()); nothing is allocated inside except what the caller
+ *    passes as `workspace` (size from the matching *_workspace_bytes query);
+ *  - all work is stream-ordered on the caller's hipStream_t (passed as void*),
+ *    no host synchronisation, graph-capturable;
+ *  - return 0 on success, a negative RQSID_E* code otherwise; the text of the
+ *    last error of the calling thread is in rqsid_last_error();
+ *  - matrices are row-major fp32 [rows][dim]; dim must be a multiple of 32.
+ */
+#ifndef RQSID_H
+#define RQSID_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RQSID_OK 0
+#define RQSID_E_ARG (-1)      /* bad argument (shape, null pointer, unsupported dim) */
+#define RQSID_E_LAUNCH (-2)   /* HIP launch / runtime error */
+#define RQSID_E_WORKSPACE (-3)
+
+/* segment flags (rqsid_assign seg_flags[s]) */
+#define RQSID_SEG_PENALTY 1u  /* empty allowed set: argmin over ALL centres of fl(d + 10000) */
+
+int rqsid_version(void);
+const char* rqsid_last_error(void);
+
+/* Centre preparation for rqsid_assign: bf16 hi/lo split of every centre in
+ * [k][dim/32][2][32] order (hi chunk then lo chunk), |c|^2 and |c| in fp32
+ * (fp64-accumulated).  Replaces the per-call centre side of torch.cdist's
+ * mm-expansion (ATen _euclidean_dist) used by pairwise_distance_full,
+ * balancekmeans/__init__.py:576-603. */
+int rqsid_prepare_centers(const float* centers, int64_t k, int32_t dim,
+                          uint16_t* c_split, float* c_sqnorm, float* c_norm, void* stream);
+
+/* Counting sort of rows by segment key (keys in [0, n_segments)).
+ * Outputs seg_row_off[S+1], seg_tile_off[S+1] (exclusive scan of
+ * ceil(rows_in_segment / tile_rows)), row_index[n] (rows grouped by key).
+ * Replaces the per-parent torch.where/mask loops of
+ * hierarchical_rq_kmeans.py:711,880-885,1210-1216 and
+ * simplified_semantic_id_generator.py:112,154-158,263. */
+int64_t rqsid_bucket_workspace_bytes(int64_t n, int32_t n_segments);
+int rqsid_bucket(const int32_t* keys, int64_t n, int32_t n_segments, int32_t tile_rows,
+                 int32_t* seg_row_off, int32_t* seg_tile_off, int32_t* row_index,
+                 void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Rows per work tile of rqsid_assign (the tile_rows to pass to rqsid_bucket). */
+int32_t rqsid_assign_tile_rows(void);
+
+/* Segmented nearest-centre assignment (exact argmin, lowest index on ties).
+ *
+ * Segment s owns rows row_index[seg_row_off[s] .. seg_row_off[s+1]) (row_index
+ * NULL = identity) and candidates j = 0 .. cand_count[s]-1 whose global centre
+ * index is cand_idx[cand_base[s]+j] (cand_idx NULL: cand_base[s]+j).
+ * out_local[row] = j of the nearest allowed centre, out_global[row] = its global
+ * index.  Segments flagged RQSID_SEG_PENALTY reproduce the reference's +10000
+ * mask with an empty allowed set (argmin over all n_centers of fl32(d)+10000);
+ * their out_local is -1.
+ *
+ * Replaces pairwise_distance_full + torch.argmin (balancekmeans/__init__.py:
+ * 489-534, 576-603), the +10000-masked reassignment/prediction of
+ * hierarchical_rq_kmeans.py:839-966,1146-1305 and the +inf-masked ones of
+ * simplified_semantic_id_generator.py:145-161,305-331.
+ *
+ * Method: bf16x3 MFMA screening with a rigorous per-candidate error bound, then
+ * an fp64 re-score of every row whose bound admits more than one candidate. */
+int64_t rqsid_assign_workspace_bytes(int64_t n_rows);
+int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row_index,
+                 int32_t n_segments, const int32_t* seg_row_off, const int32_t* seg_tile_off,
+                 int64_t max_tiles,
+                 const float* centers, const uint16_t* c_split, const float* c_sqnorm,
+                 const float* c_norm, int32_t n_centers,
+                 const int32_t* cand_base, const int32_t* cand_count, int32_t cand_count_max,
+                 const int32_t* cand_idx, const uint8_t* seg_flags,
+                 int32_t* out_local, int32_t* out_global,
+                 void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Residual r = x - c[center_id[row]]; with normalize != 0 each dimension group
+ * g is divided by (||r_g|| + 1e-8).  Replaces _compute_residuals_with_centers
+ * (hierarchical_rq_kmeans.py:1088-1128) and the plain residuals of
+ * simplified_semantic_id_generator.py:78-96,164-168. */
+int rqsid_residual(const float* x, int64_t n, int32_t dim, const float* centers, int32_t n_centers,
+                   const int32_t* center_id, const int32_t* group_dims, int32_t n_groups,
+                   int32_t normalize, float* out, void* stream);
+
+/* y = x * w_g per dimension group (hierarchical_rq_kmeans.py:583-604). */
+int rqsid_scale_groups(const float* x, int64_t n, int32_t dim, const int32_t* group_dims,
+                       int32_t n_groups, const float* weights, float* out, void* stream);
+
+/* Lloyd centroid update, first half: per-cluster fp64 sums over the rows of
+ * each segment (bucketed by rqsid_bucket with rqsid_centroid_tile_rows()).
+ * sums must be zeroed by the caller.  Replaces the per-cluster
+ * nonzero/index_select/mean loop of balancekmeans/__init__.py:315-324,434-443. */
+int32_t rqsid_centroid_tile_rows(void);
+int rqsid_centroid_accumulate(const float* x, int32_t dim, const int32_t* row_index,
+                              int32_t n_segments, const int32_t* seg_row_off,
+                              const int32_t* seg_tile_off, int64_t max_tiles,
+                              double* sums, void* stream);
+/* Second half: centers[k] = fp32(sums[k] / count[k]) for count[k] > 0 (others
+ * untouched; the caller fills empty clusters exactly as the reference does). */
+int rqsid_centroid_finalize(const double* sums, const int32_t* seg_row_off, int32_t k,
+                            int32_t dim, float* centers, void* stream);
+
+/* Match matrix (uint8 [groups][n_cand], 1 = allowed) to candidate lists:
+ * cand_count[g] = row popcount, cand_base[g] = exclusive scan, cand_idx = allowed
+ * columns in ascending order (so the local index IS the remapped id of
+ * _merge_match_matrix_cluster_ids, hierarchical_rq_kmeans.py:1055-1086),
+ * seg_flags[g] = RQSID_SEG_PENALTY for empty rows. cand_idx needs
+ * groups*n_cand entries of room. */
+int64_t rqsid_match_workspace_bytes(int32_t groups);
+int rqsid_match_to_candidates(const uint8_t* match, int32_t groups, int32_t n_cand,
+                              int32_t* cand_base, int32_t* cand_count, int32_t* cand_idx,
+                              uint8_t* seg_flags, void* workspace, int64_t workspace_bytes,
+                              void* stream);
+
+/* Dense distance matrix out[n][k] = sqrt(max(|x|^2 + |c|^2 - 2 x.c, 0)) in fp32
+ * (torch.cdist semantics, pairwise_distance_full balancekmeans/__init__.py:576-603),
+ * feeding the balanced auction. */
+int rqsid_pairwise_distance(const float* x, int64_t n, int32_t dim, const float* centers,
+                            int32_t k, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RQSID_H */

@@ -1,0 +1,353 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.  Never imported by the product package.
+
+A CPU (numpy) restatement of the reference hot path, used as the checker by
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg.
+Every function cites the reference file:line it restates
+(paths relative to /root/reference/src/semantic_id_generator/).
+
+Pinning: the restatement is checked against golden vectors captured by running
+the reference itself in the build container (``tests/golden/make_golden.py``,
+fixtures ``tests/golden/*.npz``; see tests/test_oracle_golden.py).
+
+Arithmetic: distances follow torch.cdist's matrix-multiply expansion in fp32
+(``sqrt(clamp(|x|^2 + |c|^2 - 2 x.c, 0))``, ATen ``_euclidean_dist``) with a
+first-index argmin, exactly the structure the reference runs; summation order
+inside BLAS differs from MKL/oneDNN, so two nearly tied centres (relative gap
+< ~1e-6) may be ordered differently — ``near_tie`` classifies such rows in fp64.
+"""
+from __future__ import annotations
+
+import json
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+F32 = np.float32
+
+
+# ---------------------------------------------------------------------------
+# distances / argmin
+# ---------------------------------------------------------------------------
+def cdist_f32(x: np.ndarray, c: np.ndarray) -> np.ndarray:
+    """balancekmeans/__init__.py:576-603 pairwise_distance_full -> torch.cdist (mm expansion)."""
+    x = x.astype(F32, copy=False)
+    c = c.astype(F32, copy=False)
+    xn = np.einsum("ij,ij->i", x, x, dtype=F32)[:, None]
+    cn = np.einsum("ij,ij->i", c, c, dtype=F32)[None, :]
+    d2 = (F32(-2.0) * x) @ c.T + xn + cn
+    return np.sqrt(np.maximum(d2, F32(0.0)), dtype=F32)
+
+
+def exact_d2(x: np.ndarray, c: np.ndarray) -> np.ndarray:
+    """fp64 squared distances (the arbiter for near ties)."""
+    x = x.astype(np.float64)
+    c = c.astype(np.float64)
+    return (x * x).sum(1)[:, None] + (c * c).sum(1)[None, :] - 2.0 * (x @ c.T)
+
+
+def _dist(x: np.ndarray, c: np.ndarray, exact: bool) -> np.ndarray:
+    """fp32 cdist (the reference's arithmetic) or, with exact=True, fp64 squared distances:
+    the argmin of the latter is the exact nearest centre, which is what the HIP kernels
+    return (lowest index on exact ties)."""
+    return exact_d2(x, c) if exact else cdist_f32(x, c)
+
+
+def nearest(x: np.ndarray, c: np.ndarray, chunk: int = 65536, exact: bool = False) -> np.ndarray:
+    """KMeans.predict (balancekmeans/__init__.py:489-534): argmin of cdist, first index on ties."""
+    out = np.empty(len(x), dtype=np.int64)
+    for i in range(0, len(x), chunk):
+        out[i:i + chunk] = _dist(x[i:i + chunk], c, exact).argmin(1)
+    return out
+
+
+def segmented_nearest(x: np.ndarray, c: np.ndarray, seg: np.ndarray, allowed: List[np.ndarray],
+                      penalty: str = "10000", exact: bool = False) -> np.ndarray:
+    """Masked argmin of hierarchical_rq_kmeans.py:876-890 / :942-952 / :1207-1221 / :1274-1288
+    and simplified_semantic_id_generator.py:149-161 / :319-328.
+
+    Row i may only take centres ``allowed[seg[i]]`` (global indices, ascending).  With the
+    hierarchical ``+10000*(1-mask)`` the masked-out centres can never win while the
+    allowed distances stay below 10000 (always true for normalised residuals), so the
+    restatement computes the restricted argmin directly; an EMPTY allowed set reproduces
+    ``argmin(fl32(d + 10000))`` over every centre. Returns global indices."""
+    out = np.empty(len(x), dtype=np.int64)
+    order = np.argsort(seg, kind="stable")
+    bounds = np.searchsorted(seg[order], np.arange(len(allowed) + 1))
+    for s in range(len(allowed)):
+        rows = order[bounds[s]:bounds[s + 1]]
+        if len(rows) == 0:
+            continue
+        a = allowed[s]
+        if len(a) == 0:
+            if penalty == "inf":
+                out[rows] = 0  # argmin over an all-inf row
+            else:
+                if exact:
+                    d = np.sqrt(np.maximum(exact_d2(x[rows], c), 0).astype(F32)).astype(F32)
+                else:
+                    d = cdist_f32(x[rows], c)
+                out[rows] = (d + F32(10000.0)).argmin(1)
+            continue
+        out[rows] = a[_dist(x[rows], c[a], exact).argmin(1)]
+    return out
+
+
+def near_tie(x: np.ndarray, c: np.ndarray, a: np.ndarray, b: np.ndarray, rel: float = 1e-6) -> np.ndarray:
+    """True where centres a[i] and b[i] are within ``rel`` (relative, fp64) of each other for row i."""
+    x = x.astype(np.float64)
+    da = ((x - c[a].astype(np.float64)) ** 2).sum(1)
+    db = ((x - c[b].astype(np.float64)) ** 2).sum(1)
+    return np.abs(np.sqrt(da) - np.sqrt(db)) <= rel * np.maximum(np.sqrt(np.maximum(da, db)), 1e-30)
+
+
+# ---------------------------------------------------------------------------
+# residuals / weights
+# ---------------------------------------------------------------------------
+def residual(x: np.ndarray, c: np.ndarray, ids: np.ndarray, group_dims: Sequence[int] = (),
+             normalize: bool = True) -> np.ndarray:
+    """_compute_residuals_with_centers (hierarchical_rq_kmeans.py:1088-1128): r = x - c[id]; per
+    dimension group r_g /= (||r_g|| + 1e-8) in fp32.  normalize=False: simplified :78-96.
+    The norm is taken in fp64 and rounded once (torch's fp32 reduction may differ by 1 ulp)."""
+    r = (x.astype(F32) - c.astype(F32)[ids]).astype(F32)
+    if not normalize:
+        return r
+    gd = list(group_dims) or [x.shape[1]]
+    s = 0
+    for g in gd:
+        blk = r[:, s:s + g]
+        n = np.sqrt((blk.astype(np.float64) ** 2).sum(1, keepdims=True)).astype(F32)
+        r[:, s:s + g] = blk / (n + F32(1e-8))
+        s += g
+    return r
+
+
+def apply_weights(x: np.ndarray, group_dims: Sequence[int], weights: Sequence[float]) -> np.ndarray:
+    """_apply_weights (hierarchical_rq_kmeans.py:583-604)."""
+    w = np.concatenate([np.full(g, wv, dtype=F32) for g, wv in zip(group_dims, weights)])
+    return (x.astype(F32) * w[None, :]).astype(F32)
+
+
+# ---------------------------------------------------------------------------
+# multi-level encode
+# ---------------------------------------------------------------------------
+def match_allowed(match: np.ndarray) -> List[np.ndarray]:
+    return [np.nonzero(row)[0] for row in np.asarray(match)]
+
+
+def merge_match_ids(match: np.ndarray, raw: np.ndarray, before: np.ndarray) -> np.ndarray:
+    """_merge_match_matrix_cluster_ids (hierarchical_rq_kmeans.py:1055-1086): rank of the raw
+    column among the group's allowed columns; a column outside the allowed set raises KeyError."""
+    m = np.asarray(match) == 1
+    rank = np.cumsum(m, axis=1) - 1
+    ok = m[before, raw]
+    if not ok.all():
+        i = int(np.nonzero(~ok)[0][0])
+        raise KeyError(int(raw[i]))
+    return rank[before, raw].astype(np.int64)
+
+
+def encode(x: np.ndarray, centers: Sequence[np.ndarray], need: Sequence[int],
+           match: Optional[np.ndarray] = None, group_dims: Sequence[int] = (),
+           weights: Optional[Sequence[Sequence[float]]] = None, *, normalize: bool = True,
+           match_lookup: bool = True, residual_global_id: bool = True, remap_last: bool = True,
+           last_group_mult: str = "need_l_minus_2", residual_from_weighted: bool = False,
+           exact: bool = False) -> np.ndarray:
+    """HierarchicalRQKMeans.predict (hierarchical_rq_kmeans.py:539-581, levels :1146-1305) and the
+    training-time reassignment it mirrors (:839-966); simplified path with normalize=False,
+    remap_last=False, last_group_mult='need_minus_2' (simplified :145-172, :305-331).
+    Flags as in generative_ranking_recommender_amd.encode.LevelSemantics."""
+    L = len(centers)
+    d = x.shape[1]
+    gd = list(group_dims) or [d]
+    cur = x.astype(F32)
+    ids: List[np.ndarray] = []
+    for l in range(L):
+        w = cur if weights is None else apply_weights(cur, gd, weights[l])
+        c = np.asarray(centers[l], dtype=F32)
+        if l == 0:
+            glob = nearest(w, c, exact=exact)
+            out = glob
+        elif l < L - 1:
+            prev = ids[l - 1]
+            nb = need[l]
+            allowed = [np.arange(p * nb, (p + 1) * nb) for p in range(need[l - 1])]
+            glob = segmented_nearest(w, c, prev, allowed, penalty="10000" if normalize else "inf", exact=exact)
+            out = glob % nb
+        else:
+            if match_lookup:
+                mult = need[l - 2] if last_group_mult == "need_l_minus_2" else need[-2]
+                before = ids[l - 2] * mult + ids[l - 1]
+                allowed = match_allowed(match)
+                if before.max() >= len(allowed):
+                    raise IndexError("before-id out of range")
+                glob = segmented_nearest(w, c, before, allowed, penalty="10000" if normalize else "inf",
+                                         exact=exact)
+                out = merge_match_ids(match, glob, before) if remap_last else glob
+            else:
+                glob = nearest(w, c, exact=exact)
+                out = glob
+        ids.append(out.astype(np.int64))
+        if l < L - 1:
+            src = w if residual_from_weighted else cur
+            cur = residual(src, c, glob if residual_global_id else out, gd, normalize)
+    return np.stack(ids, 1)
+
+
+# ---------------------------------------------------------------------------
+# Lloyd update + balanced auction + K-Means drivers
+# ---------------------------------------------------------------------------
+def centroid_update(x: np.ndarray, assign: np.ndarray, centers: np.ndarray, randint) -> np.ndarray:
+    """balancekmeans/__init__.py:314-324: C[k] = mean(X[a==k]); empty -> X[randint(N)]
+    (``randint`` stands in for the reference's torch CPU RNG draw ``torch.randint(len(X), (1,))``)."""
+    c = centers.astype(F32).copy()
+    for k in range(len(c)):
+        sel = x[assign == k]
+        if len(sel) == 0:
+            c[k] = x[int(randint(len(x)))]
+        else:
+            c[k] = (sel.astype(np.float64).sum(0) / len(sel)).astype(F32)
+    return c
+
+
+def auction_lap_half(job_and_worker_to_score: np.ndarray, tie_rule: str = "torch") -> np.ndarray:
+    """balancekmeans/__init__.py:12-140 (return_token_to_worker=True), restated on fp16 numpy arrays.
+
+    Every fp16 operation of the reference is reproduced with one rounding per op.  The one
+    implementation-defined step is which of several EQUAL values ``torch.topk`` keeps at the
+    selection boundary (and which equal bidder ``max(dim=0)`` reports).  ``tie_rule="torch"``
+    delegates exactly those two selections to torch's CPU kernels (the third-party code the
+    reference calls; torch 2.10.0 here), which pins the oracle to the reference on tied
+    inputs too; ``tie_rule="stable"`` keeps the lowest job / worker index instead (the rule
+    the GPU kernels use, identical whenever the fp16 scores have no ties)."""
+    s = np.asarray(job_and_worker_to_score, dtype=F32)
+    num_jobs, num_workers = s.shape
+    if num_jobs < num_workers:
+        return s.argmin(1).astype(np.int64)  # :24-26
+    s16 = s.astype(np.float16)
+    spread = np.float16(s16.max().astype(F32) - s16.min().astype(F32))   # fp16 op: rounds
+    eps = np.float16(F32(spread) / F32(50.0))                             # fp16 op: rounds
+    eps = max(eps, np.float16(1e-4))
+    if np.isnan(s16).any():
+        raise Exception("NaN distance")
+    w = np.ascontiguousarray(s16.T)  # [workers, jobs]
+    jpw = num_jobs // num_workers
+    value = w.copy()
+    cost = np.zeros(num_jobs, dtype=np.float16)
+    counter = 0
+    index = None
+    jobs_without_bidder = None
+    if tie_rule == "torch":
+        import torch
+    while True:
+        if tie_rule == "torch":
+            tv, ti = torch.from_numpy(value).topk(jpw + 1, dim=1)
+            top_index = ti.numpy()
+        else:
+            order = np.lexsort((np.arange(num_jobs)[None, :].repeat(num_workers, 0), -value.astype(F32)), axis=1)
+            top_index = order[:, :jpw + 1]
+        top_values = np.take_along_axis(value, top_index, 1)
+        inc = ((top_values[:, :-1].astype(F32) - top_values[:, -1:].astype(F32)).astype(np.float16).astype(F32)
+               + F32(eps)).astype(np.float16)
+        bids = np.zeros((num_workers, num_jobs), dtype=np.float16)
+        np.put_along_axis(bids, top_index[:, :-1], inc, 1)
+        if counter < 100 and index is not None:
+            bids.reshape(-1)[index] = eps
+        if counter > 1000:
+            bids.reshape(-1)[jobs_without_bidder] = eps
+        jobs_with_bidder = np.nonzero((bids > 0).any(0))[0]
+        jobs_without_bidder = np.nonzero((bids == 0).all(0))[0]
+        sub = bids[:, jobs_with_bidder]
+        if tie_rule == "torch":
+            hb, hbr = torch.from_numpy(np.ascontiguousarray(sub)).max(dim=0)
+            high_bidders, high_bids = hbr.numpy(), hb.numpy()
+        else:
+            high_bidders = sub.argmax(0)
+            high_bids = sub[high_bidders, np.arange(len(jobs_with_bidder))]
+        if len(high_bidders) == num_jobs:
+            return high_bidders.astype(np.int64)
+        cost[jobs_with_bidder] = (cost[jobs_with_bidder].astype(F32) + high_bids.astype(F32)).astype(np.float16)
+        value = (w.astype(F32) - cost[None, :].astype(F32)).astype(np.float16)
+        index = high_bidders * num_jobs + jobs_with_bidder
+        value.reshape(-1)[index] = w.reshape(-1)[index]
+        counter += 1
+
+
+class LegacyRNG:
+    """The reference draws init indices from numpy's global legacy RNG (np.random.choice,
+    balancekmeans/__init__.py:250-253) and empty-cluster rows from torch's CPU RNG."""
+
+    def __init__(self, np_seed: int, torch_randint):
+        self.np = np.random.RandomState(np_seed)
+        self.torch_randint = torch_randint
+
+    def choice(self, n, k):
+        return self.np.choice(n, k, replace=k > n)
+
+
+def kmeans_fit(x: np.ndarray, k: int, rng: LegacyRNG, iter_limit: int, balanced: bool, tol: float = 1e-3,
+               min_loss_target: Optional[float] = None):
+    """KMeans.fit (balancekmeans/__init__.py:368-465) and, with min_loss_target, KMeans.fit_by_min_loss
+    (:259-365).  Returns (centers, last assignment)."""
+    x = x.astype(F32)
+    c = x[rng.choice(len(x), k)].copy()
+    it = 0
+    best_loss, best_c = float("inf"), None
+    while True:
+        if min_loss_target is not None and it > 0 and it % 10 == 0:
+            c = x[rng.choice(len(x), k)].copy()
+        d = cdist_f32(x, c)
+        a = auction_lap_half(-d) if balanced else d.argmin(1)
+        prev = c.copy()
+        c = centroid_update(x, a, c, rng.torch_randint)
+        if min_loss_target is not None:
+            cnt = np.bincount(cdist_f32(x, c).argmin(1), minlength=k)
+            loss = float(np.maximum(cnt - min_loss_target, 0)[cnt > min_loss_target].sum())
+            if loss <= best_loss:
+                best_loss, best_c = loss, c.copy()
+        shift = np.sqrt(((c.astype(np.float64) - prev) ** 2).sum(1)).sum()
+        it += 1
+        if shift ** 2 < tol or (iter_limit != 0 and it >= iter_limit):
+            break
+    return (best_c if min_loss_target is not None else c), a
+
+
+def adaptive_iter_limit(num_samples: int, n_clusters: int, layer: int, base_iter_limit: int = 100,
+                        is_sub_cluster: bool = False) -> int:
+    """_calculate_adaptive_iter_limit (hierarchical_rq_kmeans.py:288-366)."""
+    spc = num_samples / max(n_clusters, 1)
+    if is_sub_cluster:
+        it = 15 if num_samples < 5000 else 20 if num_samples < 10000 else 25 if num_samples < 20000 else 30
+        if spc < 50:
+            it = max(10, int(it * 0.8))
+        elif spc > 200:
+            it = int(it * 1.2)
+        return max(10, it)
+    if num_samples < 5000:
+        it = max(10, int(base_iter_limit * 0.2))
+    elif num_samples < 10000:
+        it = max(15, int(base_iter_limit * 0.3))
+    elif num_samples < 50000:
+        it = max(30, int(base_iter_limit * 0.5))
+    elif num_samples < 100000:
+        it = max(50, int(base_iter_limit * 0.7))
+    elif num_samples < 500000:
+        it = base_iter_limit
+    elif num_samples < 1000000:
+        it = int(base_iter_limit * 1.2)
+    else:
+        it = int(base_iter_limit * 1.5)
+    if n_clusters > 512:
+        it = int(it * 1.3)
+    elif n_clusters > 256:
+        it = int(it * 1.15)
+    if layer > 1:
+        it = max(10, int(it * 0.9))
+    if spc < 50:
+        it = int(it * 1.2)
+    return max(10, it)
+
+
+def jsonl_lines(song_ids: Sequence[str], ids: np.ndarray) -> bytes:
+    """save_semantic_ids (simplified :368-385) / _save_semantic_ids (train_semantic_ids.py:239-264)."""
+    return "".join(json.dumps({"song_id": s, "semantic_ids": [int(v) for v in row]}) + "\n"
+                   for s, row in zip(song_ids, ids)).encode()

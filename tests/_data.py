@@ -1,0 +1,62 @@
+"""Regenerate the inputs of the golden fixtures (they store outputs + input sha256 only)."""
+import numpy as np
+
+from generative_ranking_recommender_amd import synth
+
+SMALL_CFG = dict(layer_clusters=[8, 16, 16], need_clusters=[8, 8, 8], embedding_dim=512, iter_limit=5)
+
+
+def checked(x, sha):
+    got = synth.sha256(x)
+    assert got == str(sha), "synthetic generator drifted from the golden capture"
+    return x
+
+
+def assign_inputs(g):
+    x = checked(synth.small_mixture(4096, m=64, seed=11), g["x_sha"])
+    c = x[g["cidx"]].copy()
+    return x, c
+
+
+def tie_inputs(x, c):
+    c2 = c.copy()
+    c2[77] = c2[5]
+    c2[100] = c2[3]
+    c2[127] = c2[0]
+    x2 = x[:512].copy()
+    x2[0], x2[1], x2[2] = c2[5], c2[3], c2[0]
+    return x2, c2
+
+
+def residual_inputs():
+    x = synth.small_mixture(4096, m=64, seed=11)
+    c = x[np.random.default_rng(5).choice(4096, 128, replace=False)].copy()
+    return x, c
+
+
+def update_inputs(g):
+    base = synth.small_mixture(256, m=8, seed=13)
+    return checked(np.concatenate([base, base[:64]], 0), g["x_sha"])
+
+
+def auction_case(g, tag):
+    return g[f"dist_{tag}"], g[f"out_{tag}"]
+
+
+def fit_inputs(g):
+    return checked(synth.small_mixture(512, m=16, seed=23), g["x_sha"])
+
+
+def small_rq_inputs(g):
+    x = checked(synth.small_mixture(2048, m=64, seed=21), g["x_sha"])
+    xn = synth.small_mixture(512, m=64, seed=22)
+    if "xn_sha" in g:
+        checked(xn, g["xn_sha"])
+    return x, xn
+
+
+def prod_encode_inputs(g):
+    cb = synth.encode_codebooks(seed=99)
+    assert synth.codebooks_sha(cb) == str(g["cb_sha"])
+    x = checked(synth.mixture_rows(0, 2000), g["x_sha"])
+    return x, cb

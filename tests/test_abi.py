@@ -1,0 +1,53 @@
+"""The C-ABI library builds for gfx950, loads, and exports every symbol include/rqsid.h declares."""
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from generative_ranking_recommender_amd import _lib
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def declared_symbols():
+    text = (REPO / "include" / "rqsid.h").read_text()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z0-9_]+\*?\s+\*?(rqsid_[a-z0-9_]+)\s*\(", text, re.M)))
+
+
+def test_header_and_binding_agree():
+    assert set(declared_symbols()) == set(_lib.SIGNATURES), "ctypes table out of sync with include/rqsid.h"
+
+
+def test_library_exports_every_declared_symbol():
+    _lib.build()
+    lib = _lib.load()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.LIB_PATH)], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (rqsid_\w+)", out))
+    assert set(declared_symbols()) <= exported
+
+
+def test_library_is_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", str(_lib.LIB_PATH)], capture_output=True,
+                         text=True)
+    blob = _lib.LIB_PATH.read_bytes()
+    assert b"gfx950" in blob
+
+
+def test_host_only_queries_need_no_gpu():
+    lib = _lib.load()
+    assert lib.rqsid_version() >= 1
+    assert lib.rqsid_assign_tile_rows() == 128
+    assert lib.rqsid_assign_workspace_bytes(1000) >= 1000 * 32
+    assert lib.rqsid_bucket_workspace_bytes(10, 16384) >= 16384 * 8
+
+
+def test_argument_errors_map_to_value_error():
+    lib = _lib.load()
+    rc = lib.rqsid_prepare_centers(None, 4, 48, None, None, None, None)  # dim not a multiple of 32
+    assert rc == -1
+    assert "prepare_centers" in lib.rqsid_last_error().decode()
+    with pytest.raises(ValueError):
+        _lib.check(rc, "rqsid_prepare_centers")

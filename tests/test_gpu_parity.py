@@ -1,0 +1,245 @@
+"""HIP kernels (through the C ABI) vs the CPU oracle and the reference's golden vectors.
+
+Bar: integer IDs bit-identical to the oracle/reference; any row where they differ
+must be a certified fp64 near tie (relative gap < 1e-6), and there are none on
+these inputs.  Floating outputs: residuals within 1 ulp of the oracle (whose norm
+is the correctly rounded one), centroids within 1e-5 relative.
+"""
+import numpy as np
+import pytest
+import torch
+
+from generative_ranking_recommender_amd import ops, synth
+from generative_ranking_recommender_amd.encode import (HIERARCHICAL_PREDICT_REFERENCE, HIERARCHICAL_TRAIN,
+                                                       SIMPLIFIED, LevelSemantics, RQEncoder)
+from oracle import rq_oracle as O
+from tests import _data
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def gpu(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def assert_ids_equal_or_near_tie(x, c, got, ref):
+    """got must be bit-identical to the oracle's exact argmin; against the fp32 (reference
+    arithmetic) oracle every difference must be a certified near tie. Returns #near ties."""
+    bad = np.nonzero(got != ref)[0]
+    if len(bad):
+        nt = O.near_tie(x[bad], c, got[bad], ref[bad])
+        assert nt.all(), f"{(~nt).sum()} non-tie mismatches out of {len(got)}"
+    return len(bad)
+
+
+def exact_ids(x, c):
+    return O.nearest(x, c, exact=True)
+
+
+def test_nearest_golden(golden):
+    g = golden("assign")
+    x, c = _data.assign_inputs(g)
+    got = ops.nearest(gpu(x), ops.prepare_centers(gpu(c))).cpu().numpy()
+    assert (got == g["ids"]).all()
+
+
+def test_nearest_ties_lowest_index(golden):
+    g = golden("assign")
+    x, c = _data.assign_inputs(g)
+    x2, c2 = _data.tie_inputs(x, c)
+    ws = ops.AssignWorkspace(len(x2), DEV)
+    got = ops.nearest(gpu(x2), ops.prepare_centers(gpu(c2)), workspace=ws).cpu().numpy()
+    assert (got == g["ids_tie"]).all()
+    assert ws.rescored() >= 3  # exact duplicates can only be separated by the fp64 re-score
+
+
+@pytest.mark.parametrize("n,k,d", [(1, 8, 512), (129, 128, 512), (5000, 100, 256), (20000, 256, 512),
+                                   (3000, 1000, 64), (777, 2560, 512)])
+def test_nearest_random(n, k, d):
+    x = synth.small_mixture(n, d=d, m=50, seed=n + k)
+    c = synth.small_mixture(k, d=d, m=50, seed=n + k + 1)
+    got = ops.nearest(gpu(x), ops.prepare_centers(gpu(c))).cpu().numpy()
+    assert (got == exact_ids(x, c)).all()
+    assert_ids_equal_or_near_tie(x, c, got, O.nearest(x, c))
+
+
+def test_nearest_forced_near_ties():
+    """Rows exactly half-way between two centres and centres 1 ulp apart: the bf16 screen cannot
+    separate them, the fp64 re-score must, with the lowest index winning exact ties."""
+    rng = np.random.default_rng(3)
+    c = rng.standard_normal((64, 512), dtype=np.float32)
+    c[10] = c[3]
+    c[11] = np.nextafter(c[4], np.float32(np.inf))
+    x = np.concatenate([(c[3] + c[20]) / 2, (c[4] + c[5]) / 2, c[3], c[4], c[11]]).reshape(5, 512).astype(np.float32)
+    x = np.concatenate([x, rng.standard_normal((300, 512), dtype=np.float32)])
+    ws = ops.AssignWorkspace(len(x), DEV)
+    got = ops.nearest(gpu(x), ops.prepare_centers(gpu(c)), workspace=ws).cpu().numpy()
+    d2 = O.exact_d2(x, c)
+    exact = d2.argmin(1)  # first index among exact ties
+    assert (got == exact).all()
+    assert got[2] == 3 and got[3] == 4 and got[4] == 11
+
+
+@pytest.mark.parametrize("gd,norm", [([512], True), ([128, 384], True), ([512], False), ([100, 12, 400], True)])
+def test_residual(gd, norm):
+    x = synth.small_mixture(3000, m=30, seed=4)
+    c = synth.small_mixture(64, m=30, seed=5)
+    ids = np.random.default_rng(0).integers(0, 64, 3000)
+    got = ops.residual(gpu(x), gpu(c), gpu(ids.astype(np.int32)), gd, norm).cpu().numpy()
+    ref = O.residual(x, c, ids, gd, norm)
+    if not norm:
+        assert np.array_equal(got, ref)
+    else:
+        ulp = np.abs(got.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+        assert ulp.max() <= 1 and (ulp > 0).mean() < 1e-3
+
+
+def test_residual_golden(golden):
+    g = golden("residual")
+    x, c = _data.residual_inputs()
+    for tag, gd in (("g512", [512]), ("g128_384", [128, 384])):
+        got = ops.residual(gpu(x), gpu(c), gpu(g["ids"].astype(np.int32)), gd, True).cpu().numpy()
+        np.testing.assert_allclose(got[:256], g[f"res_{tag}_head"], rtol=3e-7, atol=1e-9)
+    got = ops.residual(gpu(x), gpu(c), gpu(g["ids"].astype(np.int32)), [512], False).cpu().numpy()
+    assert np.array_equal(got[:256], g["res_plain_head"])
+
+
+def test_bucket_is_grouped_permutation():
+    keys = np.random.default_rng(1).integers(0, 300, 100000).astype(np.int32)
+    keys[:5000] = 7  # one big segment
+    b = ops.bucket(gpu(keys), 300)
+    off = b.seg_row_off.cpu().numpy()
+    idx = b.row_index.cpu().numpy()
+    assert off[0] == 0 and off[-1] == len(keys)
+    assert np.array_equal(np.diff(off), np.bincount(keys, minlength=300))
+    assert np.array_equal(np.sort(idx), np.arange(len(keys)))
+    for s in (0, 7, 299):
+        assert (keys[idx[off[s]:off[s + 1]]] == s).all()
+    toff = b.seg_tile_off.cpu().numpy()
+    assert np.array_equal(np.diff(toff), (np.diff(off) + 127) // 128)
+
+
+def test_segmented_assign_with_match_lists():
+    rng = np.random.default_rng(9)
+    n, k, groups = 30000, 640, 64
+    x = synth.small_mixture(n, m=40, seed=8)
+    c = synth.small_mixture(k, m=40, seed=9)
+    match = np.zeros((groups, k), dtype=np.uint8)
+    for gi in range(groups):
+        match[gi, rng.choice(k, 200 if gi % 5 else 256, replace=False)] = 1
+    seg = rng.integers(0, groups, n).astype(np.int32)
+    cand = ops.match_to_candidates(gpu(match))
+    b = ops.bucket(gpu(seg), groups)
+    loc, glob = ops.assign(gpu(x), ops.prepare_centers(gpu(c)), b, cand)
+    loc, glob = loc.cpu().numpy(), glob.cpu().numpy()
+    allowed = O.match_allowed(match)
+    assert (glob == O.segmented_nearest(x, c, seg, allowed, exact=True)).all()
+    assert_ids_equal_or_near_tie(x, c, glob, O.segmented_nearest(x, c, seg, allowed))
+    rank = np.cumsum(match, 1) - 1
+    assert (loc == rank[seg, glob]).all()
+
+
+def test_penalty_segment_matches_reference_rule():
+    rng = np.random.default_rng(2)
+    x = synth.small_mixture(500, m=10, seed=1)
+    c = synth.small_mixture(96, m=10, seed=2)
+    match = np.zeros((4, 96), dtype=np.uint8)
+    match[0, :32] = 1
+    match[2, 40:80] = 1  # groups 1 and 3 are empty -> +10000 everywhere
+    seg = rng.integers(0, 4, 500).astype(np.int32)
+    cand = ops.match_to_candidates(gpu(match))
+    loc, glob = ops.assign(gpu(x), ops.prepare_centers(gpu(c)), ops.bucket(gpu(seg), 4), cand)
+    glob = glob.cpu().numpy()
+    assert (glob == O.segmented_nearest(x, c, seg, O.match_allowed(match), exact=True)).all()
+    assert (loc.cpu().numpy()[np.isin(seg, [1, 3])] == -1).all()
+
+
+def test_centroid_update_matches_oracle():
+    x = synth.small_mixture(50000, m=20, seed=6)
+    a = np.random.default_rng(4).integers(0, 96, 50000)
+    a[a == 17] = 18  # an empty cluster keeps its previous centre
+    prev = synth.small_mixture(96, m=20, seed=7)
+    cen, cnt = ops.centroid_update(gpu(x), gpu(a.astype(np.int32)), 96, gpu(prev.copy()))
+    cen = cen.cpu().numpy()
+    ref = O.centroid_update(x, a, prev, lambda n: 0)
+    mask = np.bincount(a, minlength=96) > 0
+    np.testing.assert_allclose(cen[mask], ref[mask], rtol=1e-6, atol=1e-7)
+    assert np.array_equal(cen[~mask], prev[~mask])
+    assert np.array_equal(cnt.cpu().numpy(), np.bincount(a, minlength=96))
+
+
+def test_pairwise_distance():
+    x = synth.small_mixture(3000, m=30, seed=12)
+    c = synth.small_mixture(100, m=30, seed=13)
+    got = ops.pairwise_distance(gpu(x), gpu(c)).cpu().numpy().astype(np.float64)
+    ref = np.sqrt(np.maximum(O.exact_d2(x, c), 0))
+    scale = np.sqrt((x.astype(np.float64) ** 2).sum(1)[:, None] + (c.astype(np.float64) ** 2).sum(1)[None, :])
+    assert (np.abs(got ** 2 - ref ** 2) <= 4e-6 * scale ** 2).all()
+
+
+# --- multi-level encoder vs reference goldens ----------------------------------------
+def _hier_encoder(g, sem, device=DEV):
+    cents = [torch.from_numpy(g[k]) for k in ("c0", "c1", "c2")]
+    return RQEncoder(cents, _data.SMALL_CFG["need_clusters"], match=torch.from_numpy(g["match"]), semantics=sem,
+                     device=device)
+
+
+def test_encoder_hierarchical_golden(golden):
+    g = golden("hierarchical")
+    x, xn = _data.small_rq_inputs(g)
+    assert (_hier_encoder(g, HIERARCHICAL_TRAIN).encode(gpu(x)).cpu().numpy() == g["train_ids"]).all()
+    assert (_hier_encoder(g, HIERARCHICAL_PREDICT_REFERENCE).encode(gpu(x)).cpu().numpy() == g["pred_bug"]).all()
+    fix = LevelSemantics(residual_global_id=False)
+    assert (_hier_encoder(g, fix).encode(gpu(x)).cpu().numpy() == g["pred_fix"]).all()
+    assert (_hier_encoder(g, HIERARCHICAL_PREDICT_REFERENCE).encode(gpu(xn)).cpu().numpy()
+            == g["pred_new_bug"]).all()
+    if int(g["new_fix_keyerror"]) >= 0:
+        with pytest.raises(KeyError) as e:
+            _hier_encoder(g, fix).encode(gpu(xn))
+        assert e.value.args[0] == int(g["new_fix_keyerror"])
+
+
+def test_encoder_simplified_golden(golden):
+    g = golden("simplified")
+    x, _ = _data.small_rq_inputs(g)
+    cents = [torch.from_numpy(g[k]) for k in ("l0_centers", "mid_centers", "final_centers")]
+    enc = RQEncoder(cents, _data.SMALL_CFG["need_clusters"], match=torch.from_numpy(g["match"]), semantics=SIMPLIFIED,
+                    device=DEV)
+    assert (enc.encode(gpu(x)).cpu().numpy() == g["ids"]).all()
+
+
+def test_encoder_prod_shapes_golden(golden):
+    g = golden("encode_prod")
+    x, cb = _data.prod_encode_inputs(g)
+    cents = [torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")]
+    m = torch.from_numpy(cb["match"])
+    modes = {"pred_bug": HIERARCHICAL_PREDICT_REFERENCE, "pred_fix": LevelSemantics(residual_global_id=False),
+             "pred_train": HIERARCHICAL_TRAIN}
+    for key, sem in modes.items():
+        got = RQEncoder(cents, [128, 128, 256], match=m, semantics=sem, device=DEV).encode(gpu(x)).cpu().numpy()
+        bad = int((got != g[key]).any(1).sum())
+        assert bad == 0, f"{key}: {bad} rows differ from the reference"
+
+
+def test_encoder_full_size_properties():
+    """1M rows at PROD codebook shapes: IDs in range, deterministic, and a 4096-row sample
+    identical to the oracle (size-independent checks at the benchmark scale)."""
+    cb = synth.encode_codebooks(seed=99)
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], [128, 128, 256],
+                    match=torch.from_numpy(cb["match"]), semantics=HIERARCHICAL_TRAIN, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(0)
+    means = torch.from_numpy(synth.blob_means()).to(DEV)
+    n = 1_000_000
+    lab = torch.randint(0, means.shape[0], (n,), device=DEV, generator=gen)
+    x = means[lab] + 0.25 * torch.randn((n, 512), device=DEV, generator=gen)
+    a = enc.encode(x)
+    b = enc.encode(x)
+    assert torch.equal(a, b)
+    an = a.cpu().numpy()
+    assert an.min() >= 0 and (an.max(0) < np.array([128, 128, 256])).all()
+    sel = np.random.default_rng(1).choice(n, 4096, replace=False)
+    xs = x[torch.from_numpy(sel).to(DEV)].cpu().numpy()
+    ref = O.encode(xs, [cb["c0"], cb["c1"], cb["c2"]], [128, 128, 256], cb["match"], residual_from_weighted=True,
+                   exact=True)
+    assert (an[sel] == ref).all()
