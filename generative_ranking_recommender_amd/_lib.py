@@ -26,14 +26,16 @@ c_i32, c_i64, c_f32, c_vp, c_char_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_f
 SIGNATURES = {
     "rqsid_version": (c_i32, []),
     "rqsid_last_error": (c_char_p, []),
-    "rqsid_prepare_centers": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "rqsid_prepare_centers": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp]),
     "rqsid_bucket_workspace_bytes": (c_i64, [c_i64, c_i32]),
     "rqsid_bucket": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "rqsid_assign_tile_rows": (c_i32, []),
     "rqsid_assign_workspace_bytes": (c_i64, [c_i64]),
     "rqsid_assign": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_i64,
-                             c_vp, c_vp, c_vp, c_vp, c_i32,
-                             c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+                             c_vp, c_vp, c_vp, c_i32,
+                             c_vp, c_vp, c_i32, c_vp, c_vp,
+                             c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                             c_vp, c_vp, c_vp, c_i64, c_vp]),
     "rqsid_residual": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "rqsid_scale_groups": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp]),
     "rqsid_centroid_tile_rows": (c_i32, []),
@@ -42,6 +44,7 @@ SIGNATURES = {
     "rqsid_match_workspace_bytes": (c_i64, [c_i32]),
     "rqsid_match_to_candidates": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "rqsid_pairwise_distance": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp]),
+    "rqsid_mfma_probe": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
 _lib = None

@@ -87,6 +87,7 @@ class RQEncoder:
                                                      torch.full((1,), k, dtype=torch.int32, device=device), k))
         self._ws = None
         self.last_rescored = []
+        self.force_materialized = False
 
     def _workspace(self, n):
         if self._ws is None or self._ws.n_rows < n:
@@ -98,18 +99,80 @@ class RQEncoder:
             return x
         return ops.scale_groups(x, self.group_dims, self.weights[l])
 
+    @property
+    def fused(self) -> bool:
+        """Residuals computed inside the assignment kernels (no residual matrices in HBM)."""
+        return (self.L <= 3 and len(self.group_dims) == 1 and self.weights is None
+                and not self.force_materialized)
+
     def encode(self, x: torch.Tensor, count_rescored: bool = False) -> torch.Tensor:
         """x: f32 [N, D] on the device -> int32 [N, L] semantic IDs."""
         if x.dim() != 2 or x.shape[1] != self.dim:
             raise ValueError(f"Input dimension {x.shape[-1]} does not match config embedding_dim {self.dim}")
         x = x.float().contiguous()
+        if self.L == 2:
+            raise IndexError("list index out of range")  # reference: all_cluster_ids[-2] with one level
         n = x.shape[0]
         out = torch.empty((self.L, n), dtype=torch.int32, device=x.device)
         ws = self._workspace(n)
-        cur = x
         self.last_rescored = []
-        if self.L == 2:
-            raise IndexError("list index out of range")  # reference: all_cluster_ids[-2] with one level
+        if self.fused:
+            self._encode_fused(x, out, ws, count_rescored)
+        else:
+            self._encode_materialized(x, out, ws, count_rescored)
+        return out.t().contiguous()
+
+    def _last_level_buckets(self, out, l, n, device):
+        if self.sem.match_lookup:
+            mult = self.need[l - 2] if self.sem.last_group_mult == "need_l_minus_2" else self.need[-2]
+            grp = out[l - 2] * mult + out[l - 1]
+            if mult < self.need[l - 1] and int(grp.max().item()) >= self.n_groups:
+                raise IndexError(f"index {int(grp.max().item())} is out of bounds for axis 0 with size "
+                                 f"{self.n_groups}")
+            return ops.bucket(grp, self.n_groups)
+        return ops.single_segment(n, device)
+
+    def _finish_last(self, out, l, glob):
+        if not (self.sem.match_lookup and self.sem.remap_last):
+            out[l].copy_(glob)
+        elif self.has_penalty:
+            bad = torch.nonzero(out[l] < 0)
+            if bad.numel():
+                # reference: mapping_result[prev_id][cur_id] KeyError (:1084)
+                raise KeyError(int(glob[bad[0, 0]].item()))
+
+    def _encode_fused(self, x, out, ws, count_rescored):
+        n = x.shape[0]
+        dev = x.device
+        norm = self.sem.normalize_residual
+        glob0 = torch.empty(n, dtype=torch.int32, device=dev)
+        ops.assign(x, self.pcs[0], ops.single_segment(n, dev), self.cands[0], out_local=out[0], out_global=glob0,
+                   workspace=ws)
+        out[0].copy_(glob0)
+        if count_rescored:
+            self.last_rescored.append(ws.rescored())
+        if self.L == 1:
+            return
+        # the residual centre index: the raw/global id (training, :901) or predict's modded id (:1143)
+        n1 = torch.empty(n, dtype=torch.float32, device=dev) if norm else None
+        glob1 = torch.empty(n, dtype=torch.int32, device=dev)
+        b = ops.bucket(out[0], self.need[0]) if self.L == 3 else self._last_level_buckets(out, 1, n, dev)
+        fr1 = ops.FusedResidual(1, norm, self.pcs[0].centers, glob0, den_out=n1)
+        ops.assign(x, self.pcs[1], b, self.cands[1], out_local=out[1], out_global=glob1, workspace=ws, fused=fr1)
+        if count_rescored:
+            self.last_rescored.append(ws.rescored())
+        cb_idx = glob1 if self.sem.residual_global_id else out[1]
+        glob2 = torch.empty(n, dtype=torch.int32, device=dev)
+        b = self._last_level_buckets(out, 2, n, dev)
+        fr2 = ops.FusedResidual(2, norm, self.pcs[0].centers, glob0, self.pcs[1].centers, cb_idx, den_in=n1)
+        ops.assign(x, self.pcs[2], b, self.cands[2], out_local=out[2], out_global=glob2, workspace=ws, fused=fr2)
+        if count_rescored:
+            self.last_rescored.append(ws.rescored())
+        self._finish_last(out, 2, glob2)
+
+    def _encode_materialized(self, x, out, ws, count_rescored):
+        n = x.shape[0]
+        cur = x
         glob = torch.empty(n, dtype=torch.int32, device=x.device)
         for l in range(self.L):
             w = self._weighted(cur, l)
@@ -121,27 +184,12 @@ class RQEncoder:
                 b = ops.bucket(out[l - 1], self.need[l - 1])
                 ops.assign(w, self.pcs[l], b, self.cands[l], out_local=out[l], out_global=glob, workspace=ws)
             else:
-                if self.sem.match_lookup:
-                    mult = self.need[l - 2] if self.sem.last_group_mult == "need_l_minus_2" else self.need[-2]
-                    grp = out[l - 2] * mult + out[l - 1]
-                    if mult < self.need[l - 1] and int(grp.max().item()) >= self.n_groups:
-                        raise IndexError(f"index {int(grp.max().item())} is out of bounds for axis 0 with size "
-                                         f"{self.n_groups}")
-                    b = ops.bucket(grp, self.n_groups)
-                else:
-                    b = ops.single_segment(n, x.device)
+                b = self._last_level_buckets(out, l, n, x.device)
                 ops.assign(w, self.pcs[l], b, self.cands[l], out_local=out[l], out_global=glob, workspace=ws)
-                if not (self.sem.match_lookup and self.sem.remap_last):
-                    out[l].copy_(glob)
-                elif self.has_penalty:
-                    bad = torch.nonzero(out[l] < 0)
-                    if bad.numel():
-                        # reference: mapping_result[prev_id][cur_id] KeyError (:1084)
-                        raise KeyError(int(glob[bad[0, 0]].item()))
+                self._finish_last(out, l, glob)
             if count_rescored:
                 self.last_rescored.append(ws.rescored())
             if l < self.L - 1:
                 src = w if self.sem.residual_from_weighted else cur
                 cid = glob if self.sem.residual_global_id else out[l]
                 cur = ops.residual(src, self.pcs[l].centers, cid, self.group_dims, self.sem.normalize_residual)
-        return out.t().contiguous()

@@ -47,15 +47,18 @@ def centroid_tile_rows() -> int:
 
 @dataclass
 class PreparedCenters:
-    """Centres + the derived data rqsid_assign reads (bf16 hi/lo split, |c|^2, |c|)."""
+    """Centres + the derived data rqsid_assign reads (bf16 hi/lo split and bound norms)."""
     centers: torch.Tensor      # f32 [K, D]
     split: torch.Tensor        # int16 [K, D/32, 64] (bf16 bits, hi chunk then lo chunk)
-    sqnorm: torch.Tensor       # f32 [K]
-    norm: torch.Tensor         # f32 [K]
+    meta: torch.Tensor         # f32 [K, 4]: |c|^2, |c|, |c - hi - lo|, |lo|
 
     @property
     def k(self) -> int:
         return self.centers.shape[0]
+
+    @property
+    def sqnorm(self) -> torch.Tensor:
+        return self.meta[:, 0]
 
 
 def prepare_centers(c: torch.Tensor) -> PreparedCenters:
@@ -63,11 +66,10 @@ def prepare_centers(c: torch.Tensor) -> PreparedCenters:
     _require_device(c)
     k, d = c.shape
     split = torch.empty((k, d // 32, 64), dtype=torch.int16, device=c.device)
-    sq = torch.empty(k, dtype=torch.float32, device=c.device)
-    nrm = torch.empty(k, dtype=torch.float32, device=c.device)
-    _lib.check(lib().rqsid_prepare_centers(_ptr(c), k, d, _ptr(split), _ptr(sq), _ptr(nrm), _stream()),
+    meta = torch.empty((k, 4), dtype=torch.float32, device=c.device)
+    _lib.check(lib().rqsid_prepare_centers(_ptr(c), k, d, _ptr(split), _ptr(meta), _stream()),
                "rqsid_prepare_centers")
-    return PreparedCenters(c, split, sq, nrm)
+    return PreparedCenters(c, split, meta)
 
 
 @dataclass
@@ -150,9 +152,25 @@ class AssignWorkspace:
         return int(self.buf[:4].view(torch.int32).item())
 
 
+@dataclass
+class FusedResidual:
+    """On-the-fly residual chain for rqsid_assign (res_levels 1 or 2, one dimension group).
+
+    levels=1: v = x - ca[ca_idx]            (normalize: / (||v|| + 1e-8), written to den_out)
+    levels=2: v = (x - ca[ca_idx])[/den_in] - cb[cb_idx]   (normalize: / (||v|| + 1e-8))"""
+    levels: int
+    normalize: bool
+    ca: torch.Tensor
+    ca_idx: torch.Tensor
+    cb: Optional[torch.Tensor] = None
+    cb_idx: Optional[torch.Tensor] = None
+    den_in: Optional[torch.Tensor] = None
+    den_out: Optional[torch.Tensor] = None
+
+
 def assign(x: torch.Tensor, pc: PreparedCenters, buckets: Buckets, cand: Candidates,
            out_local: Optional[torch.Tensor] = None, out_global: Optional[torch.Tensor] = None,
-           workspace: Optional[AssignWorkspace] = None):
+           workspace: Optional[AssignWorkspace] = None, fused: Optional[FusedResidual] = None):
     """Exact segmented argmin. Returns (local i32[N], global i32[N])."""
     _require_device(x, pc.centers, cand.base, cand.count, cand.idx, cand.flags)
     n, d = x.shape
@@ -165,11 +183,18 @@ def assign(x: torch.Tensor, pc: PreparedCenters, buckets: Buckets, cand: Candida
         out_global = torch.empty(n, dtype=torch.int32, device=dev)
     if workspace is None or workspace.n_rows < n:
         workspace = AssignWorkspace(n, dev)
+    f = fused
+    if f is not None:
+        _require_device(f.ca, f.ca_idx, f.cb, f.cb_idx, f.den_in, f.den_out)
     _lib.check(lib().rqsid_assign(
         _ptr(x), n, d, _ptr(buckets.row_index), buckets.n_segments, _ptr(buckets.seg_row_off),
         _ptr(buckets.seg_tile_off), buckets.max_tiles,
-        _ptr(pc.centers), _ptr(pc.split), _ptr(pc.sqnorm), _ptr(pc.norm), pc.k,
+        _ptr(pc.centers), _ptr(pc.split), _ptr(pc.meta), pc.k,
         _ptr(cand.base), _ptr(cand.count), cand.count_max, _ptr(cand.idx), _ptr(cand.flags),
+        0 if f is None else f.levels, 0 if f is None else int(f.normalize),
+        None if f is None else _ptr(f.ca), None if f is None else _ptr(f.ca_idx),
+        None if f is None else _ptr(f.cb), None if f is None else _ptr(f.cb_idx),
+        None if f is None else _ptr(f.den_in), None if f is None else _ptr(f.den_out),
         _ptr(out_local), _ptr(out_global), _ptr(workspace.buf), workspace.bytes, _stream()), "rqsid_assign")
     return out_local, out_global
 

@@ -79,23 +79,33 @@ def encode_codebooks(seed: int = 99, need=(128, 128, 256), n_cand: int = 2560,
     ``c2`` = ``n_cand`` normalised level-2 residuals; ``match`` = ``need[0]*need[1]``
     rows with exactly ``need[2]`` ones among ``n_cand`` columns (the shape of
     ``_assign_last_match_matrix``, ``hierarchical_rq_kmeans.py:968-1053``).
+    Each level samples its own independent pool of rows, so no centre is the
+    residual of a row that produced a centre one level up (that would be an exact
+    zero vector, duplicated across groups).
     """
     rng = np.random.default_rng(seed)
-    pool = mixture_rows(1 << 30, (1 << 30) + pool_rows, d=d)
-    c0 = pool[rng.choice(pool_rows, need[0], replace=False)].copy()
-    a0 = _nearest(pool, c0)
-    r1 = _normalize_rows(pool - c0[a0])
+    base = 1 << 30
+    pool0 = mixture_rows(base, base + pool_rows, d=d)
+    pool1 = mixture_rows(base + pool_rows, base + 2 * pool_rows, d=d)
+    pool2 = mixture_rows(base + 2 * pool_rows, base + 3 * pool_rows, d=d)
+    c0 = pool0[rng.choice(pool_rows, need[0], replace=False)].copy()
+    a1 = _nearest(pool1, c0)
+    r1 = _normalize_rows(pool1 - c0[a1])
     c1 = np.empty((need[0] * need[1], d), dtype=np.float32)
     for p in range(need[0]):
-        members = np.nonzero(a0 == p)[0]
+        members = np.nonzero(a1 == p)[0]
+        if len(members) == 0:
+            members = np.arange(pool_rows)
         pick = rng.choice(members, need[1], replace=len(members) < need[1])
         c1[p * need[1]:(p + 1) * need[1]] = r1[pick]
+    a2 = _nearest(pool2, c0)
+    r21 = _normalize_rows(pool2 - c0[a2])
     g1 = np.empty(pool_rows, dtype=np.int64)
     for p in range(need[0]):
-        members = np.nonzero(a0 == p)[0]
+        members = np.nonzero(a2 == p)[0]
         if len(members):
-            g1[members] = p * need[1] + _nearest(r1[members], c1[p * need[1]:(p + 1) * need[1]])
-    r2 = _normalize_rows(r1 - c1[g1])
+            g1[members] = p * need[1] + _nearest(r21[members], c1[p * need[1]:(p + 1) * need[1]])
+    r2 = _normalize_rows(r21 - c1[g1])
     c2 = r2[rng.choice(pool_rows, n_cand, replace=False)].copy()
     groups = need[0] * need[1]
     match = np.zeros((groups, n_cand), dtype=np.uint8)

@@ -243,3 +243,35 @@ def test_encoder_full_size_properties():
     ref = O.encode(xs, [cb["c0"], cb["c1"], cb["c2"]], [128, 128, 256], cb["match"], residual_from_weighted=True,
                    exact=True)
     assert (an[sel] == ref).all()
+
+
+@pytest.mark.parametrize("sem_name", ["train", "predict_ref", "simplified"])
+def test_fused_residuals_equal_materialized(sem_name):
+    """The fused kernels (residual chain rebuilt inside rqsid_assign) must give the same IDs as
+    materialised residual matrices + plain assignment."""
+    sem = {"train": HIERARCHICAL_TRAIN, "predict_ref": HIERARCHICAL_PREDICT_REFERENCE, "simplified": SIMPLIFIED}[sem_name]
+    cb = synth.encode_codebooks(seed=99)
+    x = gpu(synth.mixture_rows(0, 30000))
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], [128, 128, 256],
+                    match=torch.from_numpy(cb["match"]), semantics=sem, device=DEV)
+    assert enc.fused
+    a = enc.encode(x)
+    enc.force_materialized = True
+    b = enc.encode(x)
+    assert torch.equal(a, b)
+
+
+def test_multigroup_weighted_encode_vs_oracle():
+    """group_dims [128, 384] with the reference's default weights 1/len(groups) (:56-62): the
+    materialised path (scale_groups + per-group normalised residuals) vs the oracle."""
+    cb = synth.encode_codebooks(seed=5, need=(16, 16, 32), n_cand=320, pool_rows=8192)
+    x = synth.mixture_rows(0, 6000)
+    gd, w = [128, 384], [[0.5, 0.5]] * 3
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], [16, 16, 32],
+                    match=torch.from_numpy(cb["match"]), group_dims=gd, weights=w, semantics=HIERARCHICAL_TRAIN,
+                    device=DEV)
+    assert not enc.fused
+    got = enc.encode(gpu(x)).cpu().numpy()
+    ref = O.encode(x, [cb["c0"], cb["c1"], cb["c2"]], [16, 16, 32], cb["match"], gd, w, residual_from_weighted=True,
+                   exact=True)
+    assert (got == ref).all()
