@@ -183,7 +183,7 @@ def main():
         kern["bucket"] = {"ms": round(ms["bucket"], 3)}
     dom = max((k for k in kern if k.startswith("assign")), key=lambda k: kern[k]["ms"])
     dk = kern[dom]
-    roof = {"kernel": dom + " (rqsid_assign: assign_screen_kernel + fp64 re-score)", "bound": "hbm",
+    roof = {"kernel": dom + " (rqsid_assign: assign_screen_kernel + assign_rescore_kernel)", "bound": "hbm",
             "achieved": dk["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dk["hbm_frac"],
             "traffic": None, "bytes_per_row": bytes_row}
 
@@ -206,7 +206,7 @@ def main():
                                "layer_clusters [128,1280,1280] (BASELINE configs[2]/[3])",
                    "rows_per_gpu": n, "dim": D, "need_clusters": NEED, "candidates_last_level": N_CAND,
                    "parallelism": f"rows sharded x{world}, no collective",
-                   "method": "bf16x3 MFMA screen + fp64 re-score (exact argmin)"},
+                   "method": "fp16 MFMA screen (LDS-DMA ring) + fp64 re-score (exact argmin)"},
         "roofline": roof,
         "kernels": kern,
     }

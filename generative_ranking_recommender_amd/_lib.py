@@ -1,7 +1,7 @@
 """Loader for the in-tree HIP library ``librqsid.so`` (C ABI: ``include/rqsid.h``).
 
 The product path has no CPU fallback: if the library is missing or no GPU is
-visible the calls below raise.  ``build()`` compiles ``csrc/rqsid.hip`` for
+visible the calls below raise.  ``build()`` compiles ``csrc/*.hip`` for
 gfx950 with hipcc into the package directory, so the ``.so`` travels with the
 repository snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
 """
@@ -15,7 +15,8 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 REPO = PKG.parent
 LIB_PATH = PKG / "librqsid.so"
-SRC = PKG / "csrc" / "rqsid.hip"
+SRCS = [PKG / "csrc" / "rqsid.hip", PKG / "csrc" / "assign.hip"]
+DEPS = SRCS + [PKG / "csrc" / "internal.h"]
 HEADER = REPO / "include" / "rqsid.h"
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC"]
@@ -44,7 +45,7 @@ SIGNATURES = {
     "rqsid_match_workspace_bytes": (c_i64, [c_i32]),
     "rqsid_match_to_candidates": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "rqsid_pairwise_distance": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp]),
-    "rqsid_mfma_probe": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rqsid_mfma_probe": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
 _lib = None
@@ -52,11 +53,11 @@ _lib = None
 
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile the HIP library for gfx950 (hipcc cross-compiles without a GPU)."""
-    if LIB_PATH.exists() and not force and LIB_PATH.stat().st_mtime >= max(SRC.stat().st_mtime, HEADER.stat().st_mtime):
+    if LIB_PATH.exists() and not force and LIB_PATH.stat().st_mtime >= max(f.stat().st_mtime for f in DEPS + [HEADER]):
         return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = LIB_PATH.with_suffix(".so.tmp")
-    cmd = [hipcc, *HIPCC_FLAGS, "-o", str(tmp), str(SRC)]
+    cmd = [hipcc, *HIPCC_FLAGS, "-o", str(tmp), *map(str, SRCS)]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

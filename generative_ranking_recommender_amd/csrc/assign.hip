@@ -1,0 +1,815 @@
+// assign.hip — exact segmented nearest-centre assignment for gfx950 (rqsid_assign, rqsid_prepare_centers).
+//
+// Replaces pairwise_distance_full + torch.argmin (balancekmeans/__init__.py:489-534, 576-603) and the
+// masked reassignment / prediction of hierarchical_rq_kmeans.py:839-966, 1146-1305 and
+// simplified_semantic_id_generator.py:145-161, 305-331.
+//
+// Two kernels:
+//  1. assign_screen_kernel — a segmented "grouped GEMM + argmin".  A work tile is 128 rows of ONE
+//     segment (parent cluster / (l1,l2) group) against that segment's candidate centres.  X·Cᵀ runs on
+//     v_mfma_f32_32x32x16_f16 with ONE fp16 term per operand (x rounded to fp16 on the fly, centres
+//     pre-rounded by rqsid_prepare_centers).  A rigorous per-(row, candidate) error bound, built from the
+//     exact rounding residuals |x - fp16(x)| (measured on the fly) and |c - fp16(c)| (prepared) plus a
+//     pessimistic model of the MFMA's internal accumulation, decides whether the row's nearest candidate
+//     is certain.  Rows where the bound admits several candidates go to a work list.
+//     Data movement: x rows and fp16 centre chunks stream HBM/L2 -> LDS by LDS-DMA
+//     (global_load_lds_dwordx4, issued in inline asm so hipcc does not drain it) through an S-stage ring,
+//     one barrier per 32-dim chunk; x rows are a per-lane row gather (rows are bucketed by segment).
+//     Centres are the MFMA A operand (32 candidates on M) and rows the B operand, so each lane owns ONE
+//     row and 16 of its candidates: the argmin is in-register plus one cross-half exchange.
+//  2. assign_rescore_kernel — exact fp64 re-score of the listed rows (one wave per row), rebuilding the
+//     row's vector with the reference's fp32 operation sequence.  The returned ID is therefore the exact
+//     argmin (lowest index on exact ties), independent of any summation order.
+//
+// Fused residual chain (res_levels 1/2): the vector assigned for row i of segment s is
+//     RL0: x_i      RL1: x_i - ca[seg_ca[s]]      RL2: (x_i - ca[seg_ca[s]]) [/ den_in[i]] - cb[seg_cb[s]]
+// (NORM additionally divides by ||.|| + 1e-8), i.e. _compute_residuals_with_centers
+// (hierarchical_rq_kmeans.py:1088-1128) / simplified :78-96 without materialising residual matrices.
+// The residual centres are per-SEGMENT constants (a level's segment determines the parent IDs), so
+// they are staged once per tile in LDS.
+#include <cmath>
+#include <cstdlib>
+
+#include "internal.h"
+
+namespace rqsid {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int kWaves = 4;
+constexpr int kRowsPerWave = 32;
+constexpr int kTileRows = kWaves * kRowsPerWave;  // rows per work tile
+constexpr int kChunk = 32;                         // dims per ring stage
+constexpr int kXWaveBytes = kRowsPerWave * 128;    // 4 KiB: 32 rows x 32 fp32 dims
+constexpr int kXStage = kWaves * kXWaveBytes;      // 16 KiB
+constexpr int kMaxDim = 1024;
+
+constexpr int kListPerHalf = 4;             // candidates a lane half can list exactly
+constexpr int kMaxList = 2 * kListPerHalf;   // per row
+struct WorkItem {
+  int32_t row;
+  int32_t seg;
+  int32_t n;  // >=1: explicit local candidates in cand[]; -1: every candidate; -2: penalty (all centres); -3: none
+  int32_t pad;
+  uint16_t cand[kMaxList];
+};
+static_assert(sizeof(WorkItem) == 32, "work item layout");
+
+struct AssignParams {
+  const float* x;
+  int32_t dim;
+  const int32_t* row_index;
+  int32_t n_segments;
+  const int32_t* seg_row_off;
+  const int32_t* seg_tile_off;
+  const float* centers;
+  const uint16_t* c16;   // fp16 bits [k][dim] (rqsid_prepare_centers)
+  const float* c_meta;   // float4 per centre: |c|^2, |c|, |c - c16|, |c16|
+  int32_t n_centers;
+  const int32_t* cand_base;
+  const int32_t* cand_count;
+  const int32_t* cand_idx;
+  const uint8_t* seg_flags;
+  int32_t* out_local;
+  int32_t* out_global;
+  WorkItem* work;
+  int32_t* work_count;
+  int64_t work_cap;
+  float acc_rel;
+  const float* ca;
+  const int32_t* seg_ca;
+  const float* cb;
+  const int32_t* seg_cb;
+  const float* den_in;
+  float* den_out;
+};
+
+__device__ __forceinline__ int cand_global(const AssignParams& p, int base, int local) {
+  return p.cand_idx ? p.cand_idx[base + local] : base + local;
+}
+__device__ __forceinline__ int seg_row(const int32_t* map, int s) { return map ? map[s] : s; }
+
+// fp16 operand with a rigorous residual: values outside the fp16 NORMAL range go in as 0 (their whole
+// value then lands in the measured residual), so the bound never depends on denormal/overflow handling.
+__device__ __forceinline__ _Float16 to_f16(float v) {
+  const float a = fabsf(v);
+  return (_Float16)((a >= 0x1p-14f && a < 65504.0f) ? v : 0.0f);
+}
+
+// ---------------------------------------------------------------------------
+// centre preparation
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void prepare_centers_kernel(const float* __restrict__ c, int64_t k, int dim,
+                                                              _Float16* __restrict__ c16, float4* __restrict__ meta) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= k) return;
+  const float* cr = c + row * dim;
+  double s = 0.0, se = 0.0, sh = 0.0;
+  for (int i = lane; i < dim; i += 64) {
+    const float v = cr[i];
+    const _Float16 hv = to_f16(v);
+    const double hd = (double)(float)hv;
+    const double ed = (double)v - hd;  // exact
+    c16[row * dim + i] = hv;
+    s += (double)v * (double)v;
+    se += ed * ed;
+    sh += hd * hd;
+  }
+  s = wave_sum(s);
+  se = wave_sum(se);
+  sh = wave_sum(sh);
+  if (lane == 0)  // norms rounded up slightly: they only feed the screening bound
+    meta[row] = make_float4((float)s, (float)sqrt(s) * 1.0000002f, (float)sqrt(se) * 1.0000002f,
+                            (float)sqrt(sh) * 1.0000002f);
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lds_addr(const void* ptr) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)ptr;
+}
+
+// One global_load_lds_dwordx4: every lane moves 16 B from its own global address to
+// lds_base + lane*16.  Inline asm keeps hipcc's waitcnt pass from draining the ring.
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+// wait until at most N of this wave's vector-memory ops are outstanding, drain LDS ops, barrier
+template <int N>
+__device__ __forceinline__ void wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
+template <int S, int P>
+__device__ __forceinline__ void wait_chunks(int younger) {
+  // younger = chunks issued after the one we need (uniform); each chunk is P DMA ops per wave
+  if (S >= 5 && younger >= 3) wait_barrier<(S >= 5 ? 3 * P : 0)>();
+  else if (S >= 4 && younger >= 2) wait_barrier<(S >= 4 ? 2 * P : 0)>();
+  else if (younger >= 1) wait_barrier<P>();
+  else wait_barrier<0>();
+}
+
+// ---------------------------------------------------------------------------
+// screening kernel
+// ---------------------------------------------------------------------------
+template <int NT, int S>
+struct ScreenLayout {
+  static constexpr int kCStage = NT * 32 * 64;  // NT*32 candidates x 32 fp16 dims
+  static constexpr int kStage = kXStage + kCStage;
+  static constexpr int kMeta = S * kStage;       // float2 {|c|^2, |c|} per candidate of the pass
+  static constexpr int kRatio = kMeta + NT * 32 * 8;
+  static constexpr int kRes = kRatio + 16;        // residual rows ca, cb (fp32, dim each)
+  static constexpr int bytes(int rl, int dim) { return kRes + rl * dim * 4; }
+  static constexpr int kMaxBytes = kRes + 2 * kMaxDim * 4;
+};
+
+__device__ __forceinline__ void push_work(const AssignParams& p, bool need, int lane, const WorkItem& w) {
+  const unsigned long long m = __ballot(need);
+  if (!m) return;
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(p.work_count, __popcll(m));
+  base = __shfl(base, leader);
+  if (need) {
+    const int idx = base + __popcll(m & ((1ull << lane) - 1ull));
+    if (idx < p.work_cap) p.work[idx] = w;
+  }
+}
+
+// Screening error model (DESIGN.md "Screening bound").  With v the row's vector, vh = fp16(v),
+// ex = v - vh, ch = fp16(c), ec = c - ch:
+//   |v.c - vh.ch| <= |ex||c| + |vh||ec|                       (Cauchy-Schwarz, exact norms)
+//   MFMA accumulation <= acc_rel * |vh||ch|                    (tests/test_mfma_numerics.py: each
+//      v_mfma_f32_32x32x16_f16 charged 17 truncating additions at 1 ulp of |C| + sum|products|)
+// so d^2 = |c|^2 - 2 v.c/den is known to within e_k = K |c_k| + 2^-22 |c_k|^2 with the per-row
+//   K = 2/den (|ex| + |vh| rho + acc_rel |vh| (1 + rho)) + 2 dr + 2^-21 |r|
+// (rho = the pass's largest |ec_k|/|c_k|, dr = the rounding of the reference's r = v/den).
+inline float accumulation_rel(int dim) { return (float)(((dim / 16) * 17.0 + 8.0) * std::ldexp(1.0, -23) * 1.02); }
+
+template <int NT, int S, int RL, bool NORM>
+__global__ __launch_bounds__(256, NT == 4 ? 2 : 1) void assign_screen_kernel(AssignParams p) {
+  using L = ScreenLayout<NT, S>;
+  constexpr int P = 4 + NT / 2;  // DMA ops per wave per chunk (x: 4, centres: NT/2)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, r = lane & 31;
+  // XCD-aware tile order: blocks b and b+8 share an XCD (and its L2), so give each group of 8 a
+  // contiguous run of tiles -> a segment's candidate centres stay hot in one L2 (gridDim.x % 8 == 0)
+  const int G = gridDim.x;
+  const int b = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const int nseg = p.n_segments;
+  if (b >= p.seg_tile_off[nseg]) return;
+  int lo = 0, hi = nseg;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (p.seg_tile_off[mid] <= b) lo = mid; else hi = mid;
+  }
+  const int s = lo;
+  const int t0 = p.seg_row_off[s] + (b - p.seg_tile_off[s]) * kTileRows;
+  const int nrows = min(kTileRows, p.seg_row_off[s + 1] - t0);
+  const int cnt = p.cand_count[s];
+  const int cbase = p.cand_base[s];
+  const bool penalty = p.seg_flags && (p.seg_flags[s] & RQSID_SEG_PENALTY);
+  const int dim = p.dim;
+
+  const int my_local = wave * kRowsPerWave + r;
+  const bool row_valid = my_local < nrows;
+  const int pos = t0 + (row_valid ? my_local : 0);
+  const int my_row = p.row_index ? p.row_index[pos] : pos;
+
+  if (penalty || cnt <= 0) {  // block-uniform: no barrier below is skipped by part of the block
+    WorkItem w{};
+    w.row = my_row;
+    w.seg = s;
+    w.n = penalty ? -2 : -3;
+    push_work(p, h == 0 && row_valid, lane, w);
+    return;
+  }
+
+  // DMA sources for this wave's x rows: instruction i covers rows 8i + lane/8, 16-B slot lane%8 of the
+  // LDS image holding global slot (lane%8) ^ swz(row)  (swz(row) = (row>>1)&7: conflict-free reads)
+  const float* xsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rr = 8 * i + (lane >> 3);
+    const int grow = __shfl(my_row, rr);
+    const int slot = (lane & 7) ^ ((rr >> 1) & 7);
+    xsrc[i] = p.x + (int64_t)grow * dim + slot * 4;
+  }
+  // residual rows of this segment -> LDS
+  float* lds_ca = reinterpret_cast<float*>(smem + L::kRes);
+  float* lds_cb = lds_ca + dim;
+  if (RL >= 1) {
+    const float4* a = reinterpret_cast<const float4*>(p.ca + (int64_t)seg_row(p.seg_ca, s) * dim);
+    for (int i = tid; i < dim / 4; i += 256) reinterpret_cast<float4*>(lds_ca)[i] = a[i];
+  }
+  if (RL >= 2) {
+    const float4* a = reinterpret_cast<const float4*>(p.cb + (int64_t)seg_row(p.seg_cb, s) * dim);
+    for (int i = tid; i < dim / 4; i += 256) reinterpret_cast<float4*>(lds_cb)[i] = a[i];
+  }
+  float inv1 = 1.0f;
+  if (RL >= 2 && NORM) inv1 = 1.0f / p.den_in[my_row];
+  asm volatile("" : "+v"(inv1));  // its load completes before the DMA ring starts
+
+  const uint32_t lds0 = lds_addr(smem);
+  const int nch = dim / kChunk;
+  float U = INFINITY;
+  int nlist = 0;
+  int lk[kListPerHalf];
+  float llb[kListPerHalf];
+#pragma unroll
+  for (int j = 0; j < kListPerHalf; ++j) {
+    lk[j] = -1;
+    llb[j] = INFINITY;
+  }
+  double sv2 = 0.0;            // sum v^2 in fp64 (NORM: the normalising denominator is exact)
+  float sf2 = 0.f, se2 = 0.f;  // sum v^2 (fp32, bound only), sum (v - fp16(v))^2
+  float vn = 0.f, en = 0.f, inv_den = 1.f, dr = 0.f;
+  float2* lds_meta = reinterpret_cast<float2*>(smem + L::kMeta);
+  unsigned* lds_ratio = reinterpret_cast<unsigned*>(smem + L::kRatio);
+  const f32x16 zero16 = {};
+  const int xsw = (r >> 1) & 7;  // swizzle of this lane's row in the x image
+  const int csw = (r >> 2) & 3;  // swizzle of this lane's candidate row in the centre image
+
+  const int npass = (cnt + NT * 32 - 1) / (NT * 32);
+  for (int pass = 0; pass < npass; ++pass) {
+    const int pbase = pass * NT * 32;
+    // centre DMA sources: instruction j covers candidates (wave*NT/2 + j)*16 + lane/4, slot lane%4
+    const _Float16* csrc[NT / 2];
+#pragma unroll
+    for (int j = 0; j < NT / 2; ++j) {
+      const int il = (wave * (NT / 2) + j) * 16 + (lane >> 2);
+      const int kl = pbase + il < cnt ? pbase + il : cnt - 1;
+      const int cg = cand_global(p, cbase, kl);
+      const int slot = (lane & 3) ^ ((il >> 2) & 3);
+      csrc[j] = reinterpret_cast<const _Float16*>(p.c16) + (int64_t)cg * dim + slot * 8;
+    }
+    if (tid < 2) lds_ratio[tid] = 0u;
+    __syncthreads();
+    if (tid < NT * 32) {
+      const int kl = pbase + tid < cnt ? pbase + tid : cnt - 1;
+      const float4 m = reinterpret_cast<const float4*>(p.c_meta)[cand_global(p, cbase, kl)];
+      lds_meta[tid] = make_float2(m.x, m.y);
+      // positive floats order like their bit patterns
+      atomicMax(&lds_ratio[0], __float_as_uint(m.y > 0.f ? m.z / m.y * 1.000001f : (m.z > 0.f ? INFINITY : 0.f)));
+    }
+#pragma unroll
+    for (int j = 0; j < NT / 2; ++j) asm volatile("" : "+v"(csrc[j]));
+    __syncthreads();
+
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = zero16;
+
+    auto issue = [&](int c) {
+      const uint32_t sb = lds0 + (uint32_t)((c % S) * L::kStage);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        dma16(xsrc[i] + c * kChunk, __builtin_amdgcn_readfirstlane(sb + wave * kXWaveBytes + i * 1024));
+#pragma unroll
+      for (int j = 0; j < NT / 2; ++j)
+        dma16(csrc[j] + c * kChunk, __builtin_amdgcn_readfirstlane(sb + kXStage + (wave * (NT / 2) + j) * 1024));
+    };
+    auto compute = [&](int c) {
+      const unsigned char* xb = smem + (c % S) * L::kStage + wave * kXWaveBytes + r * 128;
+      const unsigned char* cbp = smem + (c % S) * L::kStage + kXStage + r * 64;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int q0 = 4 * ks + 2 * h;
+        const float4 xa = *reinterpret_cast<const float4*>(xb + ((q0 ^ xsw) << 4));
+        const float4 xc = *reinterpret_cast<const float4*>(xb + (((q0 + 1) ^ xsw) << 4));
+        float v[8] = {xa.x, xa.y, xa.z, xa.w, xc.x, xc.y, xc.z, xc.w};
+        const int d0 = c * kChunk + 16 * ks + 8 * h;
+        if (RL >= 1) {
+          const float4 a0 = *reinterpret_cast<const float4*>(lds_ca + d0);
+          const float4 a1 = *reinterpret_cast<const float4*>(lds_ca + d0 + 4);
+          const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = v[e] - av[e];  // exact fp32, as the reference
+        }
+        if (RL >= 2) {
+          const float4 b0 = *reinterpret_cast<const float4*>(lds_cb + d0);
+          const float4 b1v = *reinterpret_cast<const float4*>(lds_cb + d0 + 4);
+          const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1v.x, b1v.y, b1v.z, b1v.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = (NORM ? v[e] * inv1 : v[e]) - bv[e];
+        }
+        f16x8 bf;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const _Float16 hv = to_f16(v[e]);
+          bf[e] = hv;
+          if (pass == 0) {
+            const float ex = v[e] - (float)hv;  // exact: the fp16 rounding residual
+            se2 = fmaf(ex, ex, se2);
+            if (NORM && RL >= 1) sv2 = fma((double)v[e], (double)v[e], sv2);
+            else sf2 = fmaf(v[e], v[e], sf2);
+          }
+        }
+        const int qa = (2 * ks + h) ^ csw;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const f16x8 af = *reinterpret_cast<const f16x8*>(cbp + t * 32 * 64 + (qa << 4));
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[t], 0, 0, 0);
+        }
+      }
+    };
+
+    // S-stage ring: chunks 0..S-2 in flight before the first compute
+#pragma unroll
+    for (int c = 0; c < S - 1; ++c)
+      if (c < nch) issue(c);
+    for (int c = 0; c < nch; ++c) {
+      wait_chunks<S, P>(min(S - 2, nch - 1 - c));  // chunk c landed (every wave), chunk c-1 fully read
+      if (c + S - 1 < nch) issue(c + S - 1);         // into the stage chunk c-1 used
+      compute(c);
+    }
+
+    if (pass == 0) {
+      const float e2 = se2 + __shfl_xor(se2, 32);
+      en = sqrtf(e2) * 1.001f + 1e-30f;
+      float nrm;
+      if (NORM && RL >= 1) {
+        const double tot = sv2 + __shfl_xor(sv2, 32);
+        nrm = (float)sqrt(tot);
+        const float den = nrm + 1e-8f;
+        inv_den = 1.0f / den;
+        if (RL == 1 && h == 0 && row_valid && p.den_out) p.den_out[my_row] = den;
+        // |r_ref - v/den| per element: RL1: the reference rounds r_i = u_i/den once;
+        // RL2: v was built with a reciprocal multiply (2 ulp of |r1| = 1) and rounded
+        dr = RL == 1 ? 2.0f * 5.97e-8f : (4.0f * 2.39e-7f * (1.0f + nrm) * inv_den + 4.0f * 5.97e-8f);
+      } else {
+        nrm = sqrtf(sf2 + __shfl_xor(sf2, 32));
+      }
+      vn = nrm * 1.0001f + 1e-30f;
+    }
+    // epilogue.  Sweep 1: the least upper bound U over the row's candidates so far.  Sweep 2: list
+    // (ascending) the candidates whose lower bound is <= U, up to kListPerHalf per lane half; U only
+    // shrinks over passes, so earlier listings are re-filtered at the end.
+    const float rho = __uint_as_float(lds_ratio[0]);
+    const float hn = vn + en;       // >= |vh|
+    const float vr = vn * inv_den;  // |r| of the row being assigned
+    const float K = 2.0f * inv_den * 1.000001f * (en + hn * rho + p.acc_rel * hn * (1.0f + rho)) + 2.0f * dr +
+                    4.8e-7f * vr;
+    const float m2 = -2.0f * inv_den;
+    const float2* meta = lds_meta + 4 * h;
+    const int kl_h = pbase + 4 * h;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int io = t * 32 + (v & 3) + 8 * (v >> 2);
+        const float2 m = meta[io];  // |c|^2, |c|
+        const float sc = fmaf(m2, acc[t][v], m.x);
+        const float e = fmaf(K, m.y, fmaf(2.39e-7f, m.x, 1e-30f));
+        U = fminf(U, kl_h + io < cnt ? sc + e : INFINITY);
+      }
+    }
+    U = fminf(U, __shfl_xor(U, 32));
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int io = t * 32 + (v & 3) + 8 * (v >> 2);
+        const int kl = kl_h + io;
+        const float2 m = meta[io];
+        const float lb = fmaf(m2, acc[t][v], m.x) - fmaf(K, m.y, fmaf(2.39e-7f, m.x, 1e-30f));
+        const bool q = kl < cnt && lb <= U;
+        if (__builtin_amdgcn_ballot_w64(q)) {  // wave-uniform skip: most candidates qualify for no row
+#pragma unroll
+          for (int j = 0; j < kListPerHalf; ++j) {
+            const bool take = q && nlist == j;
+            lk[j] = take ? kl : lk[j];
+            llb[j] = take ? lb : llb[j];
+          }
+          nlist += q ? 1 : 0;
+        }
+      }
+    }
+    __syncthreads();  // meta / ring are rewritten by the next pass
+  }
+
+  // Row decision: keep the listed candidates still within the final U; a half that listed more
+  // than kListPerHalf overflows -> re-score every candidate of the segment.
+  bool ovf = nlist > kListPerHalf || cnt > 65535;
+  int nh = 0;
+  int kk[kListPerHalf];
+#pragma unroll
+  for (int j = 0; j < kListPerHalf; ++j) {
+    const bool keep = j < nlist && llb[j] <= U;
+    kk[j] = keep ? lk[j] : -1;
+    nh += keep ? 1 : 0;
+  }
+  const bool ovf_p = __shfl_xor((int)ovf, 32) != 0;
+  const int nh_p = __shfl_xor(nh, 32);
+  int kp[kListPerHalf];
+#pragma unroll
+  for (int j = 0; j < kListPerHalf; ++j) kp[j] = __shfl_xor(kk[j], 32);
+  const int ncand = nh + nh_p;
+  const bool overflow = ovf || ovf_p || ncand == 0;
+  const bool definitive = !overflow && ncand == 1;
+  if (h == 0 && row_valid && definitive) {
+    int k = -1;
+#pragma unroll
+    for (int j = 0; j < kListPerHalf; ++j) k = max(k, max(kk[j], kp[j]));
+    p.out_local[my_row] = k;
+    p.out_global[my_row] = cand_global(p, cbase, k);
+  }
+  WorkItem w{};
+  w.row = my_row;
+  w.seg = s;
+  if (overflow) {
+    w.n = -1;
+  } else {
+    // ascending candidate list (empty slots sort last); static indexing only
+    int c8[kMaxList];
+#pragma unroll
+    for (int j = 0; j < kListPerHalf; ++j) {
+      c8[j] = kk[j] >= 0 ? kk[j] : INT_MAX;
+      c8[kListPerHalf + j] = kp[j] >= 0 ? kp[j] : INT_MAX;
+    }
+#pragma unroll
+    for (int i = 0; i < kMaxList; ++i)
+#pragma unroll
+      for (int j = 0; j < kMaxList - 1 - i; ++j) {
+        const int a = c8[j], bq = c8[j + 1];
+        c8[j] = min(a, bq);
+        c8[j + 1] = max(a, bq);
+      }
+#pragma unroll
+    for (int j = 0; j < kMaxList; ++j) w.cand[j] = (uint16_t)(c8[j] == INT_MAX ? 0xFFFF : c8[j]);
+    const int n = ncand;
+    w.n = n;
+  }
+  push_work(p, h == 0 && row_valid && !definitive, lane, w);
+}
+
+// ---------------------------------------------------------------------------
+// exact re-score
+// ---------------------------------------------------------------------------
+// One wave per listed row.  The row's vector is rebuilt with the reference's fp32 operation sequence
+// (x - ca, / n1, - cb, / n2 with n = fl(sqrt(sum^2)) + 1e-8) and held in registers, lanes over dims;
+// candidates are scored 8 at a time (coalesced 2 KB centre-row reads, fp64 sums of (v - c)^2, one
+// batched cross-lane reduction), so explicit lists cost one batch and "every candidate" / penalty rows
+// cost ceil(n/8) batches.  The winner is the lexicographic minimum (distance, local index).
+constexpr int kRescoreMaxV = kMaxDim / 256;  // float4 per lane
+constexpr int kBatch = 8;
+
+template <int RL, bool NORM>
+__global__ __launch_bounds__(256) void assign_rescore_kernel(AssignParams p) {
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nw = gridDim.x * 4;
+  const int64_t nitems_raw = *p.work_count;
+  const int64_t nitems = nitems_raw < p.work_cap ? nitems_raw : p.work_cap;
+  const int nv = p.dim / 4;
+  for (int64_t it = wid; it < nitems; it += nw) {
+    const WorkItem w = p.work[it];
+    const float* xr = p.x + (int64_t)w.row * p.dim;
+    const float* car = RL >= 1 ? p.ca + (int64_t)seg_row(p.seg_ca, w.seg) * p.dim : nullptr;
+    const float* cbr = RL >= 2 ? p.cb + (int64_t)seg_row(p.seg_cb, w.seg) * p.dim : nullptr;
+    const bool screened = w.n >= 1 || w.n == -1;  // the screen wrote den_out for these rows
+    float4 v[kRescoreMaxV];
+    double ss = 0.0;
+#pragma unroll
+    for (int m = 0; m < kRescoreMaxV; ++m) {
+      const int i = lane + 64 * m;
+      if (i < nv) {
+        float4 a = reinterpret_cast<const float4*>(xr)[i];
+        if (RL >= 1) {
+          const float4 c = reinterpret_cast<const float4*>(car)[i];
+          a = make_float4(a.x - c.x, a.y - c.y, a.z - c.z, a.w - c.w);
+        }
+        if (RL >= 2) {
+          if (NORM) {
+            const float d1 = p.den_in[w.row];
+            a = make_float4(a.x / d1, a.y / d1, a.z / d1, a.w / d1);
+          }
+          const float4 c = reinterpret_cast<const float4*>(cbr)[i];
+          a = make_float4(a.x - c.x, a.y - c.y, a.z - c.z, a.w - c.w);
+        }
+        v[m] = a;
+        ss += (double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z + (double)a.w * a.w;
+      } else {
+        v[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    if (NORM && RL >= 1) {
+      float den;
+      if (RL == 1 && p.den_out && screened) den = p.den_out[w.row];
+      else den = (float)sqrt(wave_sum(ss)) + 1e-8f;
+      if (RL == 1 && p.den_out && !screened && lane == 0) p.den_out[w.row] = den;
+#pragma unroll
+      for (int m = 0; m < kRescoreMaxV; ++m)
+        v[m] = make_float4(v[m].x / den, v[m].y / den, v[m].z / den, v[m].w / den);
+    }
+    const bool penalty = w.n == -2;
+    const bool listed = w.n >= 1;
+    const int base = p.cand_base[w.seg];
+    const int n = listed ? w.n : (penalty ? p.n_centers : (w.n == -1 ? p.cand_count[w.seg] : 0));
+    double best = INFINITY;  // penalty rows compare fl32(sqrt(fl32(d^2))) + 10000 in fp32, as the reference
+    int bj = INT_MAX;
+    for (int j0 = 0; j0 < n; j0 += kBatch) {
+      double acc[kBatch];
+      int loc[kBatch];
+#pragma unroll
+      for (int jj = 0; jj < kBatch; ++jj) {
+        const int j = j0 + jj;
+        acc[jj] = 0.0;
+        loc[jj] = j < n ? (listed ? (int)w.cand[jj] : j) : INT_MAX;
+        if (j < n) {
+          const int g = penalty ? loc[jj] : cand_global(p, base, loc[jj]);
+          const float4* cr = reinterpret_cast<const float4*>(p.centers + (int64_t)g * p.dim);
+#pragma unroll
+          for (int m = 0; m < kRescoreMaxV; ++m) {
+            const int i = lane + 64 * m;
+            if (i < nv) {
+              const float4 c = cr[i];
+              const double d0 = (double)v[m].x - c.x, d1 = (double)v[m].y - c.y, d2 = (double)v[m].z - c.z,
+                           d3 = (double)v[m].w - c.w;
+              acc[jj] += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+            }
+          }
+        }
+      }
+      // halving cross-lane reduction: 4 + 2 + 1 exchanges leave lane l holding the wave total of
+      // candidate jj(l) = 4*(l>>5) + 2*((l>>4)&1) + ((l>>3)&1) summed over its 8-lane group; 3 more
+      // exchanges finish it.  10 shuffles for 8 sums instead of 48.
+      double r4[4], r2[2], r1;
+      const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double send = b5 ? acc[j] : acc[j + 4];
+        const double keep = b5 ? acc[j + 4] : acc[j];
+        r4[j] = keep + __shfl_xor(send, 32);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const double send = b4 ? r4[j] : r4[j + 2];
+        const double keep = b4 ? r4[j + 2] : r4[j];
+        r2[j] = keep + __shfl_xor(send, 16);
+      }
+      {
+        const double send = b3 ? r2[0] : r2[1];
+        const double keep = b3 ? r2[1] : r2[0];
+        r1 = keep + __shfl_xor(send, 8);
+      }
+      r1 += __shfl_xor(r1, 4);
+      r1 += __shfl_xor(r1, 2);
+      r1 += __shfl_xor(r1, 1);
+      const int my_jj = 4 * (lane >> 5) + 2 * ((lane >> 4) & 1) + ((lane >> 3) & 1);
+      int my_loc = INT_MAX;
+#pragma unroll
+      for (int jj = 0; jj < kBatch; ++jj) my_loc = my_jj == jj ? loc[jj] : my_loc;
+      double key = r1;
+      if (penalty) key = (double)((float)sqrt((double)(float)key) + 10000.0f);
+      // lexicographic (distance, index) minimum over the batch (lanes) and the running best; a NaN
+      // distance never displaces a real one
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        const double ok = __shfl_xor(key, o);
+        const int ol = __shfl_xor(my_loc, o);
+        const bool kn = key != key, okn = ok != ok;
+        const bool take = ol != INT_MAX && (my_loc == INT_MAX || (!okn && (kn || ok < key || (ok == key && ol < my_loc))));
+        key = take ? ok : key;
+        my_loc = take ? ol : my_loc;
+      }
+      {
+        const bool kn = key != key, bn = best != best;
+        const bool take = my_loc != INT_MAX &&
+                          (bj == INT_MAX || (!kn && (bn || key < best || (key == best && my_loc < bj))));
+        if (take) {
+          best = key;
+          bj = my_loc;
+        }
+      }
+    }
+    if (lane == 0) {
+      const bool found = bj != INT_MAX;
+      p.out_local[w.row] = found && !penalty ? bj : -1;
+      p.out_global[w.row] = found ? (penalty ? bj : cand_global(p, base, bj)) : -1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MFMA numerics probe: D = A.B + C with ONE v_mfma_f32_32x32x16_{bf16,f16} (32x16 A, 16x32 B,
+// 32x32 C/D, row-major).  tests/test_mfma_numerics.py uses it to pin the accumulation model the
+// screening bound relies on.
+// ---------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+template <bool F16>
+__global__ __launch_bounds__(64) void mfma_probe_kernel(const uint16_t* __restrict__ a, const uint16_t* __restrict__ b,
+                                                        const float* __restrict__ c, float* __restrict__ d) {
+  const int l = threadIdx.x, i = l & 31, hh = l >> 5;
+  f32x16 acc;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = c[((v & 3) + 8 * (v >> 2) + 4 * hh) * 32 + i];
+  if (F16) {
+    f16x8 av, bv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      av[j] = __builtin_bit_cast(_Float16, a[i * 16 + 8 * hh + j]);
+      bv[j] = __builtin_bit_cast(_Float16, b[(8 * hh + j) * 32 + i]);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bv, acc, 0, 0, 0);
+  } else {
+    bf16x8 av, bv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      av[j] = __builtin_bit_cast(__bf16, a[i * 16 + 8 * hh + j]);
+      bv[j] = __builtin_bit_cast(__bf16, b[(8 * hh + j) * 32 + i]);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int v = 0; v < 16; ++v) d[((v & 3) + 8 * (v >> 2) + 4 * hh) * 32 + i] = acc[v];
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+template <int NT, int S>
+void set_attrs(bool* ok) {
+  const int bytes = ScreenLayout<NT, S>::kMaxBytes;
+  const void* ks[] = {(const void*)assign_screen_kernel<NT, S, 0, false>,
+                      (const void*)assign_screen_kernel<NT, S, 1, false>,
+                      (const void*)assign_screen_kernel<NT, S, 1, true>,
+                      (const void*)assign_screen_kernel<NT, S, 2, false>,
+                      (const void*)assign_screen_kernel<NT, S, 2, true>};
+  for (const void* k : ks)
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) *ok = false;
+}
+
+bool g_attr_done = false;
+int ensure_attrs() {
+  if (g_attr_done) return RQSID_OK;
+  bool ok = true;
+  set_attrs<4, 3>(&ok);
+  set_attrs<8, 4>(&ok);
+  if (!ok) return fail(RQSID_E_LAUNCH, "assign: cannot raise the dynamic LDS limit");
+  g_attr_done = true;
+  return RQSID_OK;
+}
+
+template <int NT, int S>
+void launch_screen(const AssignParams& p, int rl, bool norm, unsigned grid, hipStream_t st) {
+  const size_t lds = ScreenLayout<NT, S>::bytes(rl, p.dim);
+  if (rl == 0) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 0, false>), dim3(grid), dim3(256), lds, st, p);
+  else if (rl == 1 && norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, true>), dim3(grid), dim3(256), lds, st, p);
+  else if (rl == 1) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, false>), dim3(grid), dim3(256), lds, st, p);
+  else if (norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, true>), dim3(grid), dim3(256), lds, st, p);
+  else hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, false>), dim3(grid), dim3(256), lds, st, p);
+}
+
+}  // namespace
+}  // namespace rqsid
+
+using namespace rqsid;
+
+extern "C" {
+
+int rqsid_prepare_centers(const float* centers, int64_t k, int32_t dim, uint16_t* c16, float* c_meta,
+                          void* stream) {
+  if (!centers || !c16 || !c_meta || k < 0 || dim <= 0 || dim % kChunk || dim > kMaxDim)
+    return fail(RQSID_E_ARG, "prepare_centers: bad arguments (k=%lld dim=%d)", (long long)k, dim);
+  if (k == 0) return RQSID_OK;
+  hipLaunchKernelGGL(prepare_centers_kernel, dim3((unsigned)cdiv(k, 4)), dim3(256), 0, (hipStream_t)stream,
+                     centers, k, dim, reinterpret_cast<_Float16*>(c16), reinterpret_cast<float4*>(c_meta));
+  return check_launch("prepare_centers");
+}
+
+int32_t rqsid_assign_tile_rows(void) { return kTileRows; }
+
+int64_t rqsid_assign_workspace_bytes(int64_t n_rows) {
+  return 256 + (n_rows > 0 ? n_rows : 0) * (int64_t)sizeof(WorkItem);
+}
+
+int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row_index, int32_t n_segments,
+                 const int32_t* seg_row_off, const int32_t* seg_tile_off, int64_t max_tiles, const float* centers,
+                 const uint16_t* c16, const float* c_meta, int32_t n_centers, const int32_t* cand_base,
+                 const int32_t* cand_count, int32_t cand_count_max, const int32_t* cand_idx,
+                 const uint8_t* seg_flags, int32_t res_levels, int32_t res_normalize, const float* ca,
+                 const int32_t* seg_ca, const float* cb, const int32_t* seg_cb, const float* den_in,
+                 float* den_out, int32_t* out_local, int32_t* out_global, void* workspace,
+                 int64_t workspace_bytes, void* stream) {
+  if (dim <= 0 || dim % kChunk || dim > kMaxDim || n_rows < 0 || n_segments <= 0 || !seg_row_off ||
+      !seg_tile_off || !centers || !c16 || !c_meta || !cand_base || !cand_count || !out_local || !out_global ||
+      n_centers <= 0 || cand_count_max < 0 || max_tiles < 0 || n_rows > INT32_MAX || res_levels < 0 ||
+      res_levels > 2)
+    return fail(RQSID_E_ARG, "assign: bad arguments (n=%lld dim=%d S=%d K=%d levels=%d)", (long long)n_rows, dim,
+                n_segments, n_centers, res_levels);
+  if ((res_levels >= 1 && !ca) || (res_levels == 2 && (!cb || !seg_cb || (res_normalize && !den_in))))
+    return fail(RQSID_E_ARG, "assign: residual inputs missing for res_levels=%d", res_levels);
+  if (!workspace || workspace_bytes < rqsid_assign_workspace_bytes(n_rows))
+    return fail(RQSID_E_WORKSPACE, "assign: workspace too small");
+  if (n_rows == 0 || max_tiles == 0) return RQSID_OK;
+  if (max_tiles > INT32_MAX - 8) return fail(RQSID_E_ARG, "assign: too many tiles");
+  int rc = ensure_attrs();
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  AssignParams p{};
+  p.x = x;
+  p.dim = dim;
+  p.row_index = row_index;
+  p.n_segments = n_segments;
+  p.seg_row_off = seg_row_off;
+  p.seg_tile_off = seg_tile_off;
+  p.centers = centers;
+  p.c16 = c16;
+  p.c_meta = c_meta;
+  p.n_centers = n_centers;
+  p.cand_base = cand_base;
+  p.cand_count = cand_count;
+  p.cand_idx = cand_idx;
+  p.seg_flags = seg_flags;
+  p.out_local = out_local;
+  p.out_global = out_global;
+  p.work_count = (int32_t*)workspace;
+  p.work = (WorkItem*)((char*)workspace + 256);
+  p.work_cap = n_rows;
+  p.acc_rel = accumulation_rel(dim);
+  p.ca = ca;
+  p.seg_ca = seg_ca;
+  p.cb = cb;
+  p.seg_cb = seg_cb;
+  p.den_in = den_in;
+  p.den_out = den_out;
+  const bool norm = res_normalize != 0;
+  if (hipMemsetAsync(workspace, 0, 256, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "assign: memset");
+  const unsigned grid = (unsigned)((max_tiles + 7) / 8 * 8);  // XCD remap needs a multiple of 8
+  if (cand_count_max <= 128) launch_screen<4, 3>(p, res_levels, norm, grid, st);
+  else launch_screen<8, 4>(p, res_levels, norm, grid, st);
+  if ((rc = check_launch("assign_screen"))) return rc;
+  const dim3 g(grid_cap(cdiv(n_rows, 4), 4096));
+  if (res_levels == 0) hipLaunchKernelGGL((assign_rescore_kernel<0, false>), g, dim3(256), 0, st, p);
+  else if (res_levels == 1 && norm) hipLaunchKernelGGL((assign_rescore_kernel<1, true>), g, dim3(256), 0, st, p);
+  else if (res_levels == 1) hipLaunchKernelGGL((assign_rescore_kernel<1, false>), g, dim3(256), 0, st, p);
+  else if (norm) hipLaunchKernelGGL((assign_rescore_kernel<2, true>), g, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((assign_rescore_kernel<2, false>), g, dim3(256), 0, st, p);
+  return check_launch("assign_rescore");
+}
+
+int rqsid_mfma_probe(int32_t f16, const uint16_t* a, const uint16_t* b, const float* c, float* d, void* stream) {
+  if (!a || !b || !c || !d) return fail(RQSID_E_ARG, "mfma_probe: null argument");
+  if (f16) hipLaunchKernelGGL(mfma_probe_kernel<true>, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, c, d);
+  else hipLaunchKernelGGL(mfma_probe_kernel<false>, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, c, d);
+  return check_launch("mfma_probe");
+}
+
+}  // extern "C"

@@ -1,0 +1,31 @@
+// internal.h — shared helpers of the rqsid HIP translation units (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/rqsid.h"
+
+namespace rqsid {
+
+// error text of the calling thread (rqsid_last_error) + status helpers
+int fail(int code, const char* fmt, ...);
+int check_launch(const char* what);
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline unsigned grid_cap(int64_t want, int64_t cap) {
+  return (unsigned)(want < 1 ? 1 : (want > cap ? cap : want));
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// exclusive-scan kernel shared by bucketing and the match-list builder (rqsid.hip)
+__global__ __launch_bounds__(1024) void bucket_scan_kernel(const int32_t* __restrict__ counts, int S, int tile_rows,
+                                   int32_t* __restrict__ row_off, int32_t* __restrict__ tile_off,
+                                   int32_t* __restrict__ cursor);
+
+}  // namespace rqsid

@@ -1,7 +1,7 @@
 """Multi-level residual-quantisation encoder on the HIP kernels (the bench hot path).
 
 One ``RQEncoder`` holds the trained codebooks of every level, already prepared
-for ``rqsid_assign`` (bf16 split, norms, candidate lists), and turns an fp32
+for ``rqsid_assign`` (fp16 copy, norms, candidate lists), and turns an fp32
 [N, D] device matrix into int32 [N, L] semantic IDs with no host round trip.
 
 Level semantics:
@@ -99,11 +99,22 @@ class RQEncoder:
             return x
         return ops.scale_groups(x, self.group_dims, self.weights[l])
 
+    def _last_mult(self) -> int:
+        return self.need[self.L - 3] if self.sem.last_group_mult == "need_l_minus_2" else self.need[-2]
+
     @property
     def fused(self) -> bool:
-        """Residuals computed inside the assignment kernels (no residual matrices in HBM)."""
-        return (self.L <= 3 and len(self.group_dims) == 1 and self.weights is None
-                and not self.force_materialized)
+        """Residuals computed inside the assignment kernels (no residual matrices in HBM).
+
+        The kernels subtract per-SEGMENT residual centres, so the last level fuses only when its
+        group id ``l1*mult + l2`` determines (l1, l2), i.e. mult >= need[1] (true for every shipped
+        preset; the reference itself only makes sense there, Appendix A item 8), and only when the
+        match lookup is on (the reference-bug predict mode is one unconstrained segment)."""
+        if self.L > 3 or len(self.group_dims) != 1 or self.weights is not None or self.force_materialized:
+            return False
+        if self.L == 3 and not (self.sem.match_lookup and self._last_mult() >= self.need[1]):
+            return False
+        return True
 
     def encode(self, x: torch.Tensor, count_rescored: bool = False) -> torch.Tensor:
         """x: f32 [N, D] on the device -> int32 [N, L] semantic IDs."""
@@ -153,22 +164,35 @@ class RQEncoder:
             self.last_rescored.append(ws.rescored())
         if self.L == 1:
             return
-        # the residual centre index: the raw/global id (training, :901) or predict's modded id (:1143)
         n1 = torch.empty(n, dtype=torch.float32, device=dev) if norm else None
         glob1 = torch.empty(n, dtype=torch.int32, device=dev)
         b = ops.bucket(out[0], self.need[0]) if self.L == 3 else self._last_level_buckets(out, 1, n, dev)
-        fr1 = ops.FusedResidual(1, norm, self.pcs[0].centers, glob0, den_out=n1)
+        fr1 = ops.FusedResidual(1, norm, self.pcs[0].centers, None, den_out=n1)
         ops.assign(x, self.pcs[1], b, self.cands[1], out_local=out[1], out_global=glob1, workspace=ws, fused=fr1)
         if count_rescored:
             self.last_rescored.append(ws.rescored())
-        cb_idx = glob1 if self.sem.residual_global_id else out[1]
         glob2 = torch.empty(n, dtype=torch.int32, device=dev)
         b = self._last_level_buckets(out, 2, n, dev)
-        fr2 = ops.FusedResidual(2, norm, self.pcs[0].centers, glob0, self.pcs[1].centers, cb_idx, den_in=n1)
+        seg_ca, seg_cb = self._last_segment_rows(dev)
+        fr2 = ops.FusedResidual(2, norm, self.pcs[0].centers, seg_ca, self.pcs[1].centers, seg_cb, den_in=n1)
         ops.assign(x, self.pcs[2], b, self.cands[2], out_local=out[2], out_global=glob2, workspace=ws, fused=fr2)
         if count_rescored:
             self.last_rescored.append(ws.rescored())
         self._finish_last(out, 2, glob2)
+
+    def _last_segment_rows(self, dev):
+        """Per-group residual centre rows of the last level: group g = l1*mult + l2 subtracts
+        c0[l1] and c1[l1*need1 + l2] (training / raw id, :901) or c1[l2] (predict's modded id, :1143)."""
+        key = (str(dev), self.sem.residual_global_id)
+        if getattr(self, "_seg_rows_key", None) != key:
+            mult, n1 = self._last_mult(), self.need[1]
+            g = torch.arange(self.n_groups, dtype=torch.int64, device=dev)
+            l1, l2 = g // mult, (g % mult).clamp(max=n1 - 1)
+            seg_ca = l1.clamp(max=self.pcs[0].k - 1).to(torch.int32)
+            cb = l1 * n1 + l2 if self.sem.residual_global_id else l2
+            seg_cb = cb.clamp(max=self.pcs[1].k - 1).to(torch.int32)
+            self._seg_rows, self._seg_rows_key = (seg_ca, seg_cb), key
+        return self._seg_rows
 
     def _encode_materialized(self, x, out, ws, count_rescored):
         n = x.shape[0]

@@ -47,10 +47,10 @@ def centroid_tile_rows() -> int:
 
 @dataclass
 class PreparedCenters:
-    """Centres + the derived data rqsid_assign reads (bf16 hi/lo split and bound norms)."""
+    """Centres + the derived data rqsid_assign reads (fp16 copy and screening-bound norms)."""
     centers: torch.Tensor      # f32 [K, D]
-    split: torch.Tensor        # int16 [K, D/32, 64] (bf16 bits, hi chunk then lo chunk)
-    meta: torch.Tensor         # f32 [K, 4]: |c|^2, |c|, |c - hi - lo|, |lo|
+    c16: torch.Tensor          # int16 [K, D] (IEEE half bits; out-of-normal-range values stored as 0)
+    meta: torch.Tensor         # f32 [K, 4]: |c|^2, |c|, |c - c16|, |c16|
 
     @property
     def k(self) -> int:
@@ -65,11 +65,11 @@ def prepare_centers(c: torch.Tensor) -> PreparedCenters:
     c = c.float().contiguous()
     _require_device(c)
     k, d = c.shape
-    split = torch.empty((k, d // 32, 64), dtype=torch.int16, device=c.device)
+    c16 = torch.empty((k, d), dtype=torch.int16, device=c.device)
     meta = torch.empty((k, 4), dtype=torch.float32, device=c.device)
-    _lib.check(lib().rqsid_prepare_centers(_ptr(c), k, d, _ptr(split), _ptr(meta), _stream()),
+    _lib.check(lib().rqsid_prepare_centers(_ptr(c), k, d, _ptr(c16), _ptr(meta), _stream()),
                "rqsid_prepare_centers")
-    return PreparedCenters(c, split, meta)
+    return PreparedCenters(c, c16, meta)
 
 
 @dataclass
@@ -155,15 +155,17 @@ class AssignWorkspace:
 @dataclass
 class FusedResidual:
     """On-the-fly residual chain for rqsid_assign (res_levels 1 or 2, one dimension group).
+    The subtracted centres are per SEGMENT s (the segment of a level determines its parents):
 
-    levels=1: v = x - ca[ca_idx]            (normalize: / (||v|| + 1e-8), written to den_out)
-    levels=2: v = (x - ca[ca_idx])[/den_in] - cb[cb_idx]   (normalize: / (||v|| + 1e-8))"""
+    levels=1: v = x - ca[seg_ca[s]]            (normalize: / (||v|| + 1e-8), written to den_out)
+    levels=2: v = (x - ca[seg_ca[s]])[/den_in] - cb[seg_cb[s]]   (normalize: / (||v|| + 1e-8))
+    seg_ca None = identity (segment s subtracts ca[s])."""
     levels: int
     normalize: bool
     ca: torch.Tensor
-    ca_idx: torch.Tensor
+    seg_ca: Optional[torch.Tensor] = None
     cb: Optional[torch.Tensor] = None
-    cb_idx: Optional[torch.Tensor] = None
+    seg_cb: Optional[torch.Tensor] = None
     den_in: Optional[torch.Tensor] = None
     den_out: Optional[torch.Tensor] = None
 
@@ -185,15 +187,15 @@ def assign(x: torch.Tensor, pc: PreparedCenters, buckets: Buckets, cand: Candida
         workspace = AssignWorkspace(n, dev)
     f = fused
     if f is not None:
-        _require_device(f.ca, f.ca_idx, f.cb, f.cb_idx, f.den_in, f.den_out)
+        _require_device(f.ca, f.seg_ca, f.cb, f.seg_cb, f.den_in, f.den_out)
     _lib.check(lib().rqsid_assign(
         _ptr(x), n, d, _ptr(buckets.row_index), buckets.n_segments, _ptr(buckets.seg_row_off),
         _ptr(buckets.seg_tile_off), buckets.max_tiles,
-        _ptr(pc.centers), _ptr(pc.split), _ptr(pc.meta), pc.k,
+        _ptr(pc.centers), _ptr(pc.c16), _ptr(pc.meta), pc.k,
         _ptr(cand.base), _ptr(cand.count), cand.count_max, _ptr(cand.idx), _ptr(cand.flags),
         0 if f is None else f.levels, 0 if f is None else int(f.normalize),
-        None if f is None else _ptr(f.ca), None if f is None else _ptr(f.ca_idx),
-        None if f is None else _ptr(f.cb), None if f is None else _ptr(f.cb_idx),
+        None if f is None else _ptr(f.ca), None if f is None else _ptr(f.seg_ca),
+        None if f is None else _ptr(f.cb), None if f is None else _ptr(f.seg_cb),
         None if f is None else _ptr(f.den_in), None if f is None else _ptr(f.den_out),
         _ptr(out_local), _ptr(out_global), _ptr(workspace.buf), workspace.bytes, _stream()), "rqsid_assign")
     return out_local, out_global

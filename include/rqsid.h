@@ -38,14 +38,13 @@ extern "C" {
 int rqsid_version(void);
 const char* rqsid_last_error(void);
 
-/* Centre preparation for rqsid_assign: bf16 hi/lo split of every centre in
- * [k][dim/32][2][32] order (hi chunk then lo chunk) and c_meta[k][4] =
- * {|c|^2, |c|, |c - hi - lo|, |lo|} (fp64-accumulated; the last three feed the
- * screening error bound).  Replaces the per-call centre side of torch.cdist's
- * mm-expansion (ATen _euclidean_dist) used by pairwise_distance_full,
- * balancekmeans/__init__.py:576-603. */
+/* Centre preparation for rqsid_assign: every centre rounded to fp16 (values outside the fp16
+ * normal range stored as 0) in c16 [k][dim] (IEEE half bits), and c_meta[k][4] =
+ * {|c|^2, |c|, |c - c16|, |c16|} (fp64-accumulated; the last three feed the screening error
+ * bound).  Replaces the per-call centre side of torch.cdist's mm-expansion (ATen
+ * _euclidean_dist) used by pairwise_distance_full, balancekmeans/__init__.py:576-603. */
 int rqsid_prepare_centers(const float* centers, int64_t k, int32_t dim,
-                          uint16_t* c_split, float* c_meta, void* stream);
+                          uint16_t* c16, float* c_meta, void* stream);
 
 /* Counting sort of rows by segment key (keys in [0, n_segments)).
  * Outputs seg_row_off[S+1], seg_tile_off[S+1] (exclusive scan of
@@ -76,28 +75,29 @@ int32_t rqsid_assign_tile_rows(void);
  * hierarchical_rq_kmeans.py:839-966,1146-1305 and the +inf-masked ones of
  * simplified_semantic_id_generator.py:145-161,305-331.
  *
- * Fused residuals (res_levels; dim must be a multiple of 64 and <= 1024, one
- * dimension group): the vector assigned for row i is
+ * Fused residuals (res_levels 1/2, one dimension group): the vector assigned for row i of
+ * segment s is
  *   0: x_i
- *   1: u = x_i - ca[ca_idx[i]]            [ / (||u|| + 1e-8), written to den_out[i] ]
- *   2: v = (x_i - ca[ca_idx[i]])[/den_in[i]] - cb[cb_idx[i]]   [ / (||v|| + 1e-8) ]
- * exactly the fp32 operation sequence of _compute_residuals_with_centers
- * (hierarchical_rq_kmeans.py:1088-1128, res_normalize=1) or of the simplified
- * generator's plain residuals (:91,167, res_normalize=0), without materialising
- * the residual matrix.
+ *   1: u = x_i - ca[seg_ca[s]]             [ / (||u|| + 1e-8), written to den_out[i] ]
+ *   2: v = (x_i - ca[seg_ca[s]])[/den_in[i]] - cb[seg_cb[s]]   [ / (||v|| + 1e-8) ]
+ * (seg_ca NULL = identity), exactly the fp32 operation sequence of
+ * _compute_residuals_with_centers (hierarchical_rq_kmeans.py:1088-1128, res_normalize=1) or of
+ * the simplified generator's plain residuals (:91,167, res_normalize=0), without materialising
+ * the residual matrix.  The residual centres are per SEGMENT: a level's segment (parent cluster,
+ * (l1,l2) group) determines the parent IDs whose centres are subtracted.
  *
- * Method: bf16x3 MFMA screening with a rigorous per-candidate error bound, then
- * an fp64 re-score of every row whose bound admits more than one candidate. */
+ * Method: fp16 MFMA screening (v_mfma_f32_32x32x16_f16) with a rigorous per-candidate error
+ * bound, then an fp64 re-score of every row whose bound admits more than one candidate. */
 int64_t rqsid_assign_workspace_bytes(int64_t n_rows);
 int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row_index,
                  int32_t n_segments, const int32_t* seg_row_off, const int32_t* seg_tile_off,
                  int64_t max_tiles,
-                 const float* centers, const uint16_t* c_split, const float* c_meta,
+                 const float* centers, const uint16_t* c16, const float* c_meta,
                  int32_t n_centers,
                  const int32_t* cand_base, const int32_t* cand_count, int32_t cand_count_max,
                  const int32_t* cand_idx, const uint8_t* seg_flags,
                  int32_t res_levels, int32_t res_normalize,
-                 const float* ca, const int32_t* ca_idx, const float* cb, const int32_t* cb_idx,
+                 const float* ca, const int32_t* seg_ca, const float* cb, const int32_t* seg_cb,
                  const float* den_in, float* den_out,
                  int32_t* out_local, int32_t* out_global,
                  void* workspace, int64_t workspace_bytes, void* stream);
@@ -146,10 +146,11 @@ int rqsid_match_to_candidates(const uint8_t* match, int32_t groups, int32_t n_ca
 int rqsid_pairwise_distance(const float* x, int64_t n, int32_t dim, const float* centers,
                             int32_t k, float* out, void* stream);
 
-/* Numerics probe (self-test): d = a.b + c with one v_mfma_f32_32x32x16_bf16;
- * a bf16 [32][16], b bf16 [16][32], c/d fp32 [32][32], row-major.  The tests use it
- * to pin the MFMA accumulation model behind rqsid_assign's screening bound. */
-int rqsid_mfma_probe(const uint16_t* a, const uint16_t* b, const float* c, float* d, void* stream);
+/* Numerics probe (self-test): d = a.b + c with ONE v_mfma_f32_32x32x16_f16 (f16 != 0) or
+ * _bf16; a [32][16], b [16][32] (half / bfloat16 bits), c/d fp32 [32][32], row-major.  The tests
+ * use it to pin the MFMA accumulation model behind rqsid_assign's screening bound. */
+int rqsid_mfma_probe(int32_t f16, const uint16_t* a, const uint16_t* b, const float* c, float* d,
+                     void* stream);
 
 #ifdef __cplusplus
 }

@@ -245,11 +245,13 @@ def test_encoder_full_size_properties():
     assert (an[sel] == ref).all()
 
 
-@pytest.mark.parametrize("sem_name", ["train", "predict_ref", "simplified"])
+@pytest.mark.parametrize("sem_name", ["train", "predict_fix", "simplified"])
 def test_fused_residuals_equal_materialized(sem_name):
     """The fused kernels (residual chain rebuilt inside rqsid_assign) must give the same IDs as
-    materialised residual matrices + plain assignment."""
-    sem = {"train": HIERARCHICAL_TRAIN, "predict_ref": HIERARCHICAL_PREDICT_REFERENCE, "simplified": SIMPLIFIED}[sem_name]
+    materialised residual matrices + plain assignment.  (The reference-bug predict mode has an
+    unconstrained last level and always runs materialised.)"""
+    sem = {"train": HIERARCHICAL_TRAIN, "predict_fix": LevelSemantics(residual_global_id=False),
+           "simplified": SIMPLIFIED}[sem_name]
     cb = synth.encode_codebooks(seed=99)
     x = gpu(synth.mixture_rows(0, 30000))
     enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], [128, 128, 256],
