@@ -15,7 +15,7 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 REPO = PKG.parent
 LIB_PATH = PKG / "librqsid.so"
-SRCS = [PKG / "csrc" / "rqsid.hip", PKG / "csrc" / "assign.hip"]
+SRCS = [PKG / "csrc" / "rqsid.hip", PKG / "csrc" / "assign.hip", PKG / "csrc" / "auction.hip"]
 DEPS = SRCS + [PKG / "csrc" / "internal.h"]
 HEADER = REPO / "include" / "rqsid.h"
 
@@ -45,6 +45,10 @@ SIGNATURES = {
     "rqsid_match_workspace_bytes": (c_i64, [c_i32]),
     "rqsid_match_to_candidates": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "rqsid_pairwise_distance": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp]),
+    "rqsid_auction_scores": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp]),
+    "rqsid_auction_workspace_bytes": (c_i64, [c_i64, c_i32]),
+    "rqsid_auction_lap_half": (c_i32, [c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "rqsid_greedy_match": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "rqsid_mfma_probe": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 

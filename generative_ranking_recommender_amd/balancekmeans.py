@@ -1,0 +1,202 @@
+"""Balanced K-Means on MI355X — the module API of the reference's ``balancekmeans`` package
+(src/semantic_id_generator/balancekmeans/__init__.py), with every arithmetic step on the HIP
+kernels of ``librqsid.so``:
+
+* distances + argmin  -> ``rqsid_assign`` (exact argmin; the reference's fp32 ``torch.cdist``
+  + ``torch.argmin``, :489-534, 576-603)
+* balanced assignment -> ``rqsid_auction_scores`` + ``rqsid_auction_lap_half`` (:12-140)
+* centroid update     -> ``rqsid_centroid_accumulate/finalize`` (fp64 sums, :315-324)
+
+Host-side orchestration (RNG draws, loop control, the loss bookkeeping of ``fit_by_min_loss``)
+follows the reference statement by statement so that seeded runs draw the same numpy / torch
+random numbers in the same order: ``np.random.choice`` for initial centres (:240-256) and the
+CPU ``torch.randint`` for empty clusters (:321-322).  There is no CPU compute path: tensors are
+moved to the GPU and the kernels raise if ``librqsid.so`` or the GPU is missing.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import ops
+
+logger = logging.getLogger(__name__)
+
+
+def _device(device) -> torch.device:
+    if device is None or (isinstance(device, torch.device) and device.type == "cpu") or device == "cpu":
+        # the reference defaults to CPU; this framework has no CPU compute path
+        return torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
+    return torch.device(device)
+
+
+def _to_dev(x: torch.Tensor, device: torch.device) -> torch.Tensor:
+    if not isinstance(x, torch.Tensor):
+        x = torch.as_tensor(np.asarray(x))
+    return x.float().to(device).contiguous()
+
+
+def pairwise_distance_full(data1, data2, device=None, batch_size: int = 10000) -> torch.Tensor:
+    """balancekmeans/__init__.py:576-603: fp32 [N, K] Euclidean distances (``batch_size`` is
+    accepted for signature compatibility; the kernel streams rows itself)."""
+    dev = _device(device)
+    return ops.pairwise_distance(_to_dev(data1, dev), _to_dev(data2, dev))
+
+
+def pairwise_distance_half(data1, data2, device=None, batch_size: int = 20000) -> torch.Tensor:
+    """balancekmeans/__init__.py:536-574: fp16 [N, K] distances of the fp16-rounded operands,
+    clamped at 1e-5."""
+    dev = _device(device)
+    return (-ops.auction_scores(_to_dev(data1, dev), _to_dev(data2, dev), half=True)).t().contiguous()
+
+
+def auction_lap_half(job_and_worker_to_score: torch.Tensor, return_token_to_worker: bool = True) -> torch.Tensor:
+    """balancekmeans/__init__.py:12-140 on the GPU.  ``job_and_worker_to_score`` is N x K (= -distance).
+    Returns the worker of every job (int64, on the input's device)."""
+    s = job_and_worker_to_score
+    if not return_token_to_worker:
+        raise NotImplementedError("return_token_to_worker=False is unused by the reference's callers")
+    dev = s.device if s.device.type == "cuda" else _device(None)
+    n, k = s.shape
+    if torch.isnan(s).any():
+        raise Exception("NaN distance")  # :36-38
+    w = s.to(dev).half().t().contiguous()
+    a, rounds = ops.auction(w)
+    logger.debug("auction_lap_half: %d jobs, %d workers, %d rounds", n, k, rounds)
+    return a.long()
+
+
+def auction_lap_full(job_and_worker_to_score: torch.Tensor, return_token_to_worker: bool = True):
+    """balancekmeans/__init__.py:142-210 is only reachable through predict(balanced=True), which no
+    caller uses."""
+    raise NotImplementedError("auction_lap_full (predict(balanced=True)) is not on the semantic-ID path")
+
+
+class KMeans:
+    """balancekmeans.KMeans (:223-534): same constructor, ``fit``, ``fit_by_min_loss``, ``predict``."""
+
+    def __init__(self, n_clusters=None, cluster_centers=None, device=torch.device("cpu"), balanced=False):
+        self.n_clusters = n_clusters
+        self.cluster_centers = cluster_centers
+        self.device = _device(device)
+        self.balanced = balanced
+        self.last_auction_rounds = []
+
+    # --- persistence (npz instead of the reference's pickle, :230-239) --------------------------
+    @classmethod
+    def load(cls, path_to_file):
+        with np.load(path_to_file, allow_pickle=False) as z:
+            return cls(int(z["n_clusters"]), torch.from_numpy(z["cluster_centers"]), torch.device("cpu"),
+                       bool(z["balanced"]))
+
+    def save(self, path_to_file):
+        c = self.cluster_centers
+        np.savez(path_to_file, n_clusters=self.n_clusters, balanced=self.balanced,
+                 cluster_centers=c.detach().cpu().numpy() if isinstance(c, torch.Tensor) else np.asarray(c))
+
+    # --- reference steps -------------------------------------------------------------------------
+    def initialize(self, X: torch.Tensor) -> torch.Tensor:
+        """:240-256 — np.random.choice over rows (with replacement only when K > N)."""
+        num_samples = len(X)
+        if self.n_clusters > num_samples:
+            indices = np.random.choice(num_samples, self.n_clusters, replace=True)
+        else:
+            indices = np.random.choice(num_samples, self.n_clusters, replace=False)
+        return X[torch.from_numpy(np.asarray(indices)).to(X.device)].clone()
+
+    def _check_distance(self, distance):
+        if distance != "euclidean":
+            raise NotImplementedError(f"distance={distance!r}: only 'euclidean' is on the semantic-ID path")
+
+    def _assign(self, X: torch.Tensor, half: bool) -> torch.Tensor:
+        if self.balanced:
+            a, rounds = ops.auction(ops.auction_scores(X, self.cluster_centers, half=half))
+            self.last_auction_rounds.append(rounds)
+            return a
+        return ops.nearest(X, ops.prepare_centers(self.cluster_centers))
+
+    def _update(self, X: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
+        """:314-324 — per-cluster means; an empty cluster takes X[torch.randint(len(X), (1,))] (CPU RNG,
+        drawn in cluster order exactly as the reference's loop does)."""
+        prev = self.cluster_centers.clone()
+        centers, counts = ops.centroid_update(X, a, self.n_clusters, self.cluster_centers)
+        empty = torch.nonzero(counts == 0).flatten().cpu().tolist()
+        for index in empty:
+            centers[index] = X[torch.randint(len(X), (1,))].reshape(-1)
+        self.cluster_centers = centers
+        return prev
+
+    @staticmethod
+    def _shift(c: torch.Tensor, prev: torch.Tensor) -> float:
+        return float(torch.sum(torch.sqrt(torch.sum((c - prev) ** 2, dim=1))).item())
+
+    def fit_by_min_loss(self, X, target_nodes_num, distance="euclidean", tol=1e-3, tqdm_flag=True, iter_limit=0,
+                        gamma_for_soft_dtw=0.001, half=False, online=False, iter_k=None):
+        """:259-365 — Lloyd / auction iterations, re-initialised every 10 iterations, keeping the centres
+        of the smallest overflow loss sum(max(0, count - target)) (``<=``: the latest of equal losses)."""
+        self._check_distance(distance)
+        X = _to_dev(X, self.device)
+        if not online or (online and iter_k == 0):
+            self.cluster_centers = self.initialize(X)
+        self.cluster_centers = self.cluster_centers.float().to(self.device).contiguous()
+        iteration = 0
+        min_loss, best = float("inf"), None
+        while True:
+            if iteration > 0 and iteration % 10 == 0:
+                self.cluster_centers = self.initialize(X)
+            a = self._assign(X, half)
+            prev = self._update(X, a)
+            counts = torch.bincount(ops.nearest(X, ops.prepare_centers(self.cluster_centers)).long(),
+                                    minlength=self.n_clusters)
+            over = counts - target_nodes_num
+            cur_loss = float(over[over > 0].sum().item()) if (over > 0).any() else 0
+            logger.debug("fit_by_min_loss: iteration %d loss %s", iteration, cur_loss)
+            if cur_loss <= min_loss:
+                min_loss = cur_loss
+                best = self.cluster_centers.clone()
+            center_shift = self._shift(self.cluster_centers, prev)
+            iteration += 1
+            if center_shift ** 2 < tol:
+                break
+            if iter_limit != 0 and iteration >= iter_limit:
+                break
+        self.cluster_centers = best
+        return None
+
+    def fit(self, X, distance="euclidean", tol=1e-3, tqdm_flag=True, iter_limit=0, gamma_for_soft_dtw=0.001,
+            half=False, online=False, iter_k=None):
+        """:368-465 — returns the last assignment (int64, CPU) like the reference."""
+        self._check_distance(distance)
+        X = _to_dev(X, self.device)
+        if not online or (online and iter_k == 0):
+            self.cluster_centers = self.initialize(X)
+        self.cluster_centers = self.cluster_centers.float().to(self.device).contiguous()
+        iteration = 0
+        while True:
+            a = self._assign(X, half)
+            prev = self._update(X, a)
+            center_shift = self._shift(self.cluster_centers, prev)
+            iteration += 1
+            if center_shift ** 2 < tol:
+                break
+            if iter_limit != 0 and iteration >= iter_limit:
+                break
+        return a.long().cpu()
+
+    def predict(self, X, distance="euclidean", gamma_for_soft_dtw=0.001, tqdm_flag=False, return_distances=False,
+                balanced=False):
+        """:489-534 — nearest centre (exact argmin, lowest index on ties); int64 on the CPU."""
+        self._check_distance(distance)
+        if balanced:
+            raise NotImplementedError("predict(balanced=True) uses auction_lap_full, unused by the reference's callers")
+        X = _to_dev(X, self.device)
+        if X.dim() == 1:
+            X = X.unsqueeze(0)
+        c = self.cluster_centers.float().to(self.device).contiguous()
+        ids = ops.nearest(X, ops.prepare_centers(c)).long().cpu()
+        if return_distances:
+            return ids, ops.pairwise_distance(X, c)
+        return ids

@@ -316,9 +316,14 @@ __global__ __launch_bounds__(256) void match_list_kernel(const uint8_t* __restri
 // dense distance matrix (torch.cdist semantics) for the balanced auction
 // ---------------------------------------------------------------------------
 constexpr int kPdTile = 64;
+// MODE 0: out[n][k] = fp32 distance (torch.cdist, pairwise_distance_full balancekmeans/__init__.py:576-603)
+// MODE 1: out16[k][n] = fp16(-distance): the auction's worker-major score matrix (auction_lap_half(-D), :29-43)
+// MODE 2: as 1 from fp16-rounded operands with the distance rounded to fp16 and clamped at 1e-5
+//         (pairwise_distance_half, :536-574)
+template <int MODE>
 __global__ __launch_bounds__(256) void pairwise_distance_kernel(const float* __restrict__ x, int64_t n, int dim,
                                                                 const float* __restrict__ c, int k,
-                                                                float* __restrict__ out) {
+                                                                float* __restrict__ out, uint16_t* __restrict__ out16) {
   __shared__ float xs[kPdTile][33];
   __shared__ float cs[kPdTile][33];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
@@ -329,8 +334,14 @@ __global__ __launch_bounds__(256) void pairwise_distance_kernel(const float* __r
   for (int d0 = 0; d0 < dim; d0 += 32) {
     for (int i = threadIdx.x; i < kPdTile * 32; i += 256) {
       const int rr = i >> 5, dd = i & 31;
-      xs[rr][dd] = (r0 + rr < n) ? x[(r0 + rr) * dim + d0 + dd] : 0.f;
-      cs[rr][dd] = (c0 + rr < k) ? c[(int64_t)(c0 + rr) * dim + d0 + dd] : 0.f;
+      float xv = (r0 + rr < n) ? x[(r0 + rr) * dim + d0 + dd] : 0.f;
+      float cv = (c0 + rr < k) ? c[(int64_t)(c0 + rr) * dim + d0 + dd] : 0.f;
+      if (MODE == 2) {
+        xv = (float)(_Float16)xv;
+        cv = (float)(_Float16)cv;
+      }
+      xs[rr][dd] = xv;
+      cs[rr][dd] = cv;
     }
     __syncthreads();
 #pragma unroll 8
@@ -359,11 +370,87 @@ __global__ __launch_bounds__(256) void pairwise_distance_kernel(const float* __r
       const int cc = c0 + tx + 16 * j;
       if (cc >= k) continue;
       const float d2 = (-2.f * acc[i][j] + xq[i]) + cq[j];
-      out[rr * k + cc] = sqrtf(fmaxf(d2, 0.f));
+      const float d = sqrtf(fmaxf(d2, 0.f));
+      if (MODE == 0) {
+        out[rr * k + cc] = d;
+      } else if (MODE == 1) {
+        out16[(int64_t)cc * n + rr] = __builtin_bit_cast(uint16_t, (_Float16)(-d));
+      } else {
+        const _Float16 dh = (_Float16)d, lo = (_Float16)1e-5f;
+        out16[(int64_t)cc * n + rr] = __builtin_bit_cast(uint16_t, (_Float16)(-(dh < lo ? lo : dh)));
+      }
     }
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// greedy unique-nearest match rows (the match-matrix builders)
+// ---------------------------------------------------------------------------
+// One block per group g: its sub-centres s = 0..n_g-1 (rows sub_off[g]..sub_off[g+1] of dist, a
+// [total_sub][C] distance matrix) take, in order, their nearest still-unused candidate column (lowest
+// column on exact ties): hierarchical_rq_kmeans.py:1022-1038, simplified_semantic_id_generator.py:282-291.
+// match[g][c] = 1 for the chosen columns; n_sel[g] = how many were chosen (the random fill of the
+// reference runs on the host afterwards, in the reference's RNG order).
+__global__ __launch_bounds__(256) void greedy_match_kernel(const float* __restrict__ dist, const int32_t* __restrict__ sub_off,
+                                                           int C, int max_take, uint8_t* __restrict__ match,
+                                                           int32_t* __restrict__ n_sel) {
+  extern __shared__ unsigned char used[];
+  const int g = blockIdx.x;
+  const int s0 = sub_off[g], s1 = sub_off[g + 1];
+  const int take = min(s1 - s0, max_take);
+  for (int c = threadIdx.x; c < C; c += 256) used[c] = 0;
+  __shared__ float bv[4];
+  __shared__ int bi[4];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int s = 0; s < take; ++s) {
+    const float* row = dist + (int64_t)(s0 + s) * C;
+    float best = INFINITY;
+    int bc = INT_MAX;
+    for (int c = threadIdx.x; c < C; c += 256) {
+      const float v = row[c];
+      if (!used[c] && (v < best || (v == best && c < bc) || (bc == INT_MAX && !(v == v)))) {
+        best = v;
+        bc = c;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(best, o);
+      const int oc = __shfl_xor(bc, o);
+      if (oc != INT_MAX && (bc == INT_MAX || ov < best || (ov == best && oc < bc))) {
+        best = ov;
+        bc = oc;
+      }
+    }
+    if (lane == 0) {
+      bv[wv] = best;
+      bi[wv] = bc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float b = bv[0];
+      int i = bi[0];
+      for (int q = 1; q < 4; ++q)
+        if (bi[q] != INT_MAX && (i == INT_MAX || bv[q] < b || (bv[q] == b && bi[q] < i))) {
+          b = bv[q];
+          i = bi[q];
+        }
+      if (i != INT_MAX) used[i] = 1;
+    }
+    __syncthreads();
+  }
+  int cnt = 0;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    match[(int64_t)g * C + c] = used[c];
+    cnt += used[c];
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  __shared__ int tot[4];
+  if (lane == 0) tot[wv] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) n_sel[g] = tot[0] + tot[1] + tot[2] + tot[3];
+}
 
 namespace {
 bool g_attr_done = false;
@@ -500,9 +587,34 @@ int rqsid_pairwise_distance(const float* x, int64_t n, int32_t dim, const float*
   if (!x || !centers || !out || n < 0 || k <= 0 || dim <= 0 || dim % 32)
     return fail(RQSID_E_ARG, "pairwise_distance: bad arguments");
   if (n == 0) return RQSID_OK;
-  hipLaunchKernelGGL(pairwise_distance_kernel, dim3((unsigned)cdiv(n, kPdTile), (unsigned)cdiv(k, kPdTile)),
-                     dim3(256), 0, (hipStream_t)stream, x, n, dim, centers, k, out);
+  hipLaunchKernelGGL(pairwise_distance_kernel<0>, dim3((unsigned)cdiv(n, kPdTile), (unsigned)cdiv(k, kPdTile)),
+                     dim3(256), 0, (hipStream_t)stream, x, n, dim, centers, k, out, (uint16_t*)nullptr);
   return check_launch("pairwise_distance");
+}
+
+int rqsid_auction_scores(const float* x, int64_t n, int32_t dim, const float* centers, int32_t k, int32_t half,
+                         uint16_t* out_wj, void* stream) {
+  if (!x || !centers || !out_wj || n < 0 || k <= 0 || dim <= 0 || dim % 32)
+    return fail(RQSID_E_ARG, "auction_scores: bad arguments");
+  if (n == 0) return RQSID_OK;
+  const dim3 g((unsigned)cdiv(n, kPdTile), (unsigned)cdiv(k, kPdTile));
+  if (half)
+    hipLaunchKernelGGL(pairwise_distance_kernel<2>, g, dim3(256), 0, (hipStream_t)stream, x, n, dim, centers, k,
+                       (float*)nullptr, out_wj);
+  else
+    hipLaunchKernelGGL(pairwise_distance_kernel<1>, g, dim3(256), 0, (hipStream_t)stream, x, n, dim, centers, k,
+                       (float*)nullptr, out_wj);
+  return check_launch("auction_scores");
+}
+
+int rqsid_greedy_match(const float* dist, const int32_t* sub_off, int32_t groups, int32_t n_cand, int32_t max_take,
+                       uint8_t* match, int32_t* n_selected, void* stream) {
+  if (!dist || !sub_off || !match || !n_selected || groups < 0 || n_cand <= 0 || n_cand > 65536 || max_take < 0)
+    return fail(RQSID_E_ARG, "greedy_match: bad arguments (groups=%d C=%d)", groups, n_cand);
+  if (groups == 0) return RQSID_OK;
+  hipLaunchKernelGGL(greedy_match_kernel, dim3((unsigned)groups), dim3(256), (size_t)n_cand, (hipStream_t)stream, dist,
+                     sub_off, n_cand, max_take, match, n_selected);
+  return check_launch("greedy_match");
 }
 
 }  // extern "C"

@@ -1,0 +1,104 @@
+"""Input/output formats around the semantic-ID path.
+
+* ``load_song_vectors`` — the Word2Vec CSV ``song_id,v1..vD`` without header written by
+  src/common/train_word2vec.py:69-73, read with the rules of simplified_semantic_id_generator.py:38-76
+  and train_semantic_ids.py:72-131 (rows with < 2 fields skipped, non-numeric rows skipped, rows of
+  another dimension skipped, ValueError when nothing is left, values rounded to fp16 when any
+  ``layer_clusters`` entry exceeds 512).
+* ``write_semantic_ids`` — one ``json.dumps({"song_id": ..., "semantic_ids": [...]})`` line per song
+  (simplified :368-385, train_semantic_ids.py:239-264), byte-identical to the reference.
+* ``semantic_id_statistics`` / ``training_config`` — the side files training_statistics.json and
+  training_config.json of train_semantic_ids.py:266-333.
+"""
+from __future__ import annotations
+
+import csv
+import json
+import logging
+import os
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+logger = logging.getLogger(__name__)
+
+
+def load_song_vectors(path: str, embedding_dim: int, layer_clusters: Sequence[int] = (),
+                      limit: int | None = None) -> Tuple[List[str], np.ndarray]:
+    """Returns (song_ids, vectors): float16 when any layer_clusters > 512 (the reference's
+    ``.half()``), float32 otherwise."""
+    if not os.path.isfile(path):
+        raise FileNotFoundError(f"The specified data file was not found: {path}")
+    song_ids: List[str] = []
+    rows: List[np.ndarray] = []
+    with open(path, "r", encoding="utf-8") as f:
+        for i, row in enumerate(csv.reader(f)):
+            if limit and i >= limit:
+                break
+            if len(row) < 2:
+                continue
+            try:
+                embed = np.array(row[1:], dtype=np.float32)
+            except ValueError:
+                logger.warning("Skipping row for song_id %s due to non-numeric vector data.", row[0])
+                continue
+            if embed.shape[0] == embedding_dim:
+                song_ids.append(row[0])
+                rows.append(embed)
+    if not song_ids:
+        raise ValueError("No valid data with the correct embedding dimension found in the CSV file.")
+    x = np.vstack(rows)
+    if any(n > 512 for n in layer_clusters):
+        x = x.astype(np.float16)
+    return song_ids, x
+
+
+def write_song_vectors(path: str, song_ids: Sequence[str], vectors: np.ndarray) -> None:
+    """The producer's format (train_word2vec.py:69-73): ``song_id,v1,...,vD`` with repr floats."""
+    with open(path, "w", encoding="utf-8", newline="") as f:
+        w = csv.writer(f)
+        for sid, v in zip(song_ids, vectors):
+            w.writerow([sid] + [repr(float(t)) for t in v])
+
+
+def semantic_id_lines(song_ids: Sequence[str], ids: np.ndarray) -> bytes:
+    return "".join(json.dumps({"song_id": s, "semantic_ids": [int(v) for v in row]}) + "\n"
+                   for s, row in zip(song_ids, ids)).encode("utf-8")
+
+
+def write_semantic_ids(path: str, semantic_ids: Dict[str, List[int]]) -> int:
+    """Write the jsonl; returns the number of unique semantic IDs (the reference logs it)."""
+    d = os.path.dirname(path)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    unique = set()
+    with open(path, "w", encoding="utf-8") as f:
+        for song_id, sid in semantic_ids.items():
+            f.write(json.dumps({"song_id": song_id, "semantic_ids": sid}) + "\n")
+            unique.add(tuple(sid))
+    return len(unique)
+
+
+def semantic_id_statistics(semantic_ids: Dict[str, List[int]], need_clusters: Sequence[int]) -> Dict:
+    """train_semantic_ids.py:266-310 _generate_statistics."""
+    stats = {"total_songs": len(semantic_ids),
+             "unique_semantic_ids": len(set(tuple(s) for s in semantic_ids.values())),
+             "layer_statistics": []}
+    for layer in range(len(need_clusters)):
+        layer_ids = [s[layer] for s in semantic_ids.values()]
+        counts = np.bincount(layer_ids)
+        stats["layer_statistics"].append({
+            "layer": layer + 1,
+            "unique_clusters": len(set(layer_ids)),
+            "expected_clusters": need_clusters[layer],
+            "min_cluster_id": min(layer_ids),
+            "max_cluster_id": max(layer_ids),
+            "cluster_distribution": {"min": int(counts.min()), "max": int(counts.max()),
+                                     "mean": float(counts.mean()), "std": float(counts.std())},
+        })
+    return stats
+
+
+def write_json(path: str, obj) -> None:
+    with open(path, "w", encoding="utf-8") as f:
+        json.dump(obj, f, indent=2, ensure_ascii=False)

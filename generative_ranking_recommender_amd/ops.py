@@ -7,6 +7,7 @@ There is deliberately no CPU implementation: a CPU tensor or a missing
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -264,3 +265,43 @@ def pairwise_distance(x: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
     _lib.check(lib().rqsid_pairwise_distance(_ptr(x), n, d, _ptr(c), c.shape[0], _ptr(out), _stream()),
                "rqsid_pairwise_distance")
     return out
+
+
+def auction_scores(x: torch.Tensor, c: torch.Tensor, half: bool = False) -> torch.Tensor:
+    """Worker-major fp16 scores W[k][n] = -distance (the auction's input), see include/rqsid.h."""
+    c = c.float().contiguous()
+    _require_device(x, c)
+    n, d = x.shape
+    out = torch.empty((c.shape[0], n), dtype=torch.float16, device=x.device)
+    _lib.check(lib().rqsid_auction_scores(_ptr(x), n, d, _ptr(c), c.shape[0], int(half), _ptr(out), _stream()),
+               "rqsid_auction_scores")
+    return out
+
+
+def auction(scores_wj: torch.Tensor, max_rounds: int = 0):
+    """Balanced assignment on worker-major fp16 scores [K][N]. Returns (assignment i32[N], rounds)."""
+    scores_wj = scores_wj.to(torch.float16).contiguous()
+    _require_device(scores_wj)
+    k, n = scores_wj.shape
+    out = torch.empty(n, dtype=torch.int32, device=scores_wj.device)
+    wsb = int(lib().rqsid_auction_workspace_bytes(n, k))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=scores_wj.device)
+    rounds = ctypes.c_int32(0)
+    _lib.check(lib().rqsid_auction_lap_half(_ptr(scores_wj), k, n, int(max_rounds), _ptr(out), ctypes.addressof(rounds),
+                                            _ptr(ws), wsb, _stream()), "rqsid_auction_lap_half")
+    return out, int(rounds.value)
+
+
+def greedy_match(dist: torch.Tensor, sub_off: torch.Tensor, max_take: int):
+    """Greedy unique-nearest columns per group (see include/rqsid.h rqsid_greedy_match).
+    dist: f32 [total_sub, C]; sub_off: i32 [G+1].  Returns (match u8 [G, C], n_selected i32 [G])."""
+    dist = dist.float().contiguous()
+    sub_off = sub_off.to(torch.int32).contiguous()
+    _require_device(dist, sub_off)
+    g = sub_off.numel() - 1
+    c = dist.shape[1]
+    match = torch.empty((g, c), dtype=torch.uint8, device=dist.device)
+    nsel = torch.empty(max(g, 1), dtype=torch.int32, device=dist.device)
+    _lib.check(lib().rqsid_greedy_match(_ptr(dist), _ptr(sub_off), g, c, int(max_take), _ptr(match), _ptr(nsel),
+                                        _stream()), "rqsid_greedy_match")
+    return match, nsel[:g]

@@ -146,6 +146,34 @@ int rqsid_match_to_candidates(const uint8_t* match, int32_t groups, int32_t n_ca
 int rqsid_pairwise_distance(const float* x, int64_t n, int32_t dim, const float* centers,
                             int32_t k, float* out, void* stream);
 
+/* Auction score matrix: out_wj[k][n] = fp16(-||x_i - c_j||) (fp32 distances, half = 0) or
+ * -max(fp16 distance of the fp16-rounded operands, 1e-5) (half != 0), worker-major: the input of
+ * auction_lap_half(-pairwise_distance_{full,half}(X, C)), balancekmeans/__init__.py:29-43,
+ * 536-603. */
+int rqsid_auction_scores(const float* x, int64_t n, int32_t dim, const float* centers, int32_t k,
+                         int32_t half, uint16_t* out_wj, void* stream);
+
+/* Balanced assignment: the auction of balancekmeans.auction_lap_half (balancekmeans/__init__.py:
+ * 12-140, return_token_to_worker=True) on the fp16 score matrix scores_wj[K][N] (worker-major,
+ * IEEE half bits).  out_assign[j] = worker of job j.  Every fp16 operation of the reference is
+ * reproduced with one rounding; ties at the top-k boundary keep the lowest job index and equal
+ * highest bids go to the lowest worker (the reference leaves both to torch).  N < K reproduces
+ * the reference's argmin(-D) fallback.  Blocks the calling thread (one host read per round);
+ * *out_rounds = rounds run.  max_rounds <= 0: unbounded (the reference's leftover rule ends every
+ * auction by round 1002). */
+int64_t rqsid_auction_workspace_bytes(int64_t n_jobs, int32_t n_workers);
+int rqsid_auction_lap_half(const uint16_t* scores_wj, int32_t n_workers, int64_t n_jobs,
+                           int32_t max_rounds, int32_t* out_assign, int32_t* out_rounds,
+                           void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Greedy unique-nearest match rows (_assign_last_match_matrix hierarchical_rq_kmeans.py:1022-1038,
+ * _get_dynamic_match_matrix simplified_semantic_id_generator.py:282-291): group g owns rows
+ * sub_off[g]..sub_off[g+1] of dist [total][n_cand]; its first min(rows, max_take) rows each take, in
+ * order, their nearest still-unused column (lowest column on exact ties).  match [groups][n_cand]
+ * gets 1 for taken columns, n_selected[g] their count (the reference's random fill is host work). */
+int rqsid_greedy_match(const float* dist, const int32_t* sub_off, int32_t groups, int32_t n_cand,
+                       int32_t max_take, uint8_t* match, int32_t* n_selected, void* stream);
+
 /* Numerics probe (self-test): d = a.b + c with ONE v_mfma_f32_32x32x16_f16 (f16 != 0) or
  * _bf16; a [32][16], b [16][32] (half / bfloat16 bits), c/d fp32 [32][32], row-major.  The tests
  * use it to pin the MFMA accumulation model behind rqsid_assign's screening bound. */

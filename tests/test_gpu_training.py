@@ -1,0 +1,175 @@
+"""Training path on the GPU: the auction kernels bit for bit against the oracle (stable tie rule),
+K-Means fits against the oracle, and the hierarchical / simplified trainers end to end (invariants
+and train/encode consistency; the reference's balanced fits are pinned by invariants only because
+torch.topk's tie order is implementation-defined, SURVEY.md §7 hard part 3)."""
+import numpy as np
+import pytest
+import torch
+
+from generative_ranking_recommender_amd import ops, synth
+from generative_ranking_recommender_amd import io as rq_io
+from generative_ranking_recommender_amd.balancekmeans import KMeans, auction_lap_half, pairwise_distance_half
+from generative_ranking_recommender_amd.hierarchical_rq_kmeans import HierarchicalRQKMeans, HierarchicalRQKMeansConfig
+from generative_ranking_recommender_amd.simplified_semantic_id_generator import SimplifiedHierarchicalRQ
+from oracle import rq_oracle as O
+from tests import _data
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def gpu_auction(neg_dist_f16: np.ndarray):
+    w = torch.from_numpy(np.ascontiguousarray(neg_dist_f16.T)).to(DEV)
+    a, rounds = ops.auction(w)
+    return a.cpu().numpy().astype(np.int64), rounds
+
+
+@pytest.mark.parametrize("tag", ["n64k8", "n67k8", "n1000k16", "n5k8", "n96k8"])
+def test_auction_golden_inputs_match_oracle(golden, tag):
+    g = golden("auction")
+    dist, _ = _data.auction_case(g, tag)
+    scores = (-dist).astype(np.float16)
+    got, rounds = gpu_auction(scores)
+    ref = O.auction_lap_half(scores.astype(np.float32), tie_rule="stable")
+    assert (got == ref).all()
+
+
+@pytest.mark.parametrize("n,k,levels", [(200, 8, 0), (256, 8, 0), (999, 16, 7), (3000, 16, 0), (513, 32, 3)])
+def test_auction_random_and_tied_match_oracle(n, k, levels):
+    rng = np.random.default_rng(n * k)
+    d = rng.random((n, k), dtype=np.float32) * 4
+    if levels:
+        d = np.round(d * levels) / levels  # heavy ties at every top-k boundary
+    scores = (-d).astype(np.float16)
+    got, rounds = gpu_auction(scores)
+    ref = O.auction_lap_half(scores.astype(np.float32), tie_rule="stable")
+    assert (got == ref).all()
+    if n % k:
+        assert rounds == 1002  # the leftover rule ends it (Appendix A item 6)
+
+
+def test_auction_fewer_jobs_than_workers_is_farthest():
+    rng = np.random.default_rng(0)
+    d = rng.random((5, 8), dtype=np.float32)
+    s16 = (-d).astype(np.float16)
+    got, _ = gpu_auction(s16)
+    assert (got == O.auction_lap_half(s16.astype(np.float32))).all()  # argmin(-D): the farthest centre
+
+
+def test_auction_lap_half_api_and_balance():
+    x = torch.from_numpy(synth.small_mixture(4096, m=16, seed=3)).to(DEV)
+    c = x[:64].clone()
+    d = pairwise_distance_half(x, c)
+    a = auction_lap_half(-d.float())
+    assert a.shape == (4096,) and a.dtype == torch.int64
+    cnt = torch.bincount(a, minlength=64).cpu().numpy()
+    assert cnt.sum() == 4096 and cnt.max() <= 4096 // 64 + 1 and cnt.min() >= 4096 // 64 - 1
+
+
+def seeded(seed):
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+
+
+def test_kmeans_fit_unbalanced_matches_oracle(golden):
+    g = golden("fit")
+    x = _data.fit_inputs(g)
+    seeded(5)
+    km = KMeans(n_clusters=8, device=DEV, balanced=False)
+    a = km.fit(torch.from_numpy(x), iter_limit=0).numpy()
+    gen = torch.Generator().manual_seed(5)
+    rng = O.LegacyRNG(5, lambda n: torch.randint(n, (1,), generator=gen).item())
+    c_ref, a_ref = O.kmeans_fit(x, 8, rng, iter_limit=0, balanced=False)
+    assert (a == a_ref).all()
+    np.testing.assert_allclose(km.cluster_centers.cpu().numpy(), c_ref, rtol=1e-5, atol=1e-5)
+    # the reference's own golden (same seeds, torch's arithmetic)
+    assert (a == g["fit_unbal_assign"]).all()
+    np.testing.assert_allclose(km.cluster_centers.cpu().numpy(), g["fit_unbal_centers"], rtol=1e-5, atol=1e-5)
+
+
+def test_kmeans_empty_cluster_takes_random_row():
+    x = synth.small_mixture(300, m=3, seed=9)
+    seeded(1)
+    km = KMeans(n_clusters=40, device=DEV, balanced=False)
+    km.fit(torch.from_numpy(x), iter_limit=2)
+    gen = torch.Generator().manual_seed(1)
+    rng = O.LegacyRNG(1, lambda n: torch.randint(n, (1,), generator=gen).item())
+    c_ref, a_ref = O.kmeans_fit(x, 40, rng, iter_limit=2, balanced=False)
+    np.testing.assert_allclose(km.cluster_centers.cpu().numpy(), c_ref, rtol=1e-5, atol=1e-5)
+
+
+def test_kmeans_balanced_fit_invariants():
+    x = torch.from_numpy(synth.small_mixture(2048, m=16, seed=4))
+    seeded(7)
+    km = KMeans(n_clusters=16, device=DEV, balanced=True)
+    a = km.fit(x, iter_limit=4)
+    cnt = np.bincount(a.numpy(), minlength=16)
+    assert cnt.sum() == 2048 and cnt.max() <= 2048 // 16 + 1
+    seeded(7)
+    km2 = KMeans(n_clusters=16, device=DEV, balanced=True)
+    a2 = km2.fit(x, iter_limit=4)
+    assert torch.equal(a, a2) and torch.equal(km.cluster_centers, km2.cluster_centers)  # deterministic
+    seeded(8)
+    km3 = KMeans(n_clusters=16, device=DEV, balanced=True)
+    km3.fit_by_min_loss(x, target_nodes_num=64, iter_limit=12)
+    assert km3.cluster_centers.shape == (16, 512) and torch.isfinite(km3.cluster_centers).all()
+    assert len(km3.last_auction_rounds) == 12
+
+
+SMALL = dict(layer_clusters=[8, 16, 16], need_clusters=[8, 8, 8], embedding_dim=512, iter_limit=5)
+
+
+def test_hierarchical_train_predict_save_load(tmp_path):
+    x = synth.small_mixture(2048, m=64, seed=21)
+    seeded(42)
+    model = HierarchicalRQKMeans(HierarchicalRQKMeansConfig(**SMALL), checkpoint_dir=str(tmp_path / "ck"), device=DEV)
+    res = model.train(x)
+    ids = np.stack([t.cpu().numpy() for t in res["cluster_ids"]], 1)
+    assert ids.shape == (2048, 3)
+    assert (ids >= 0).all() and (ids.max(0) < np.array(SMALL["need_clusters"])).all()
+    m = np.asarray(model.match_matrices[0])
+    assert m.shape == (64, 32) and (m.sum(1)[np.unique(ids[:, 0] * 8 + ids[:, 1])] == 8).all()
+    # the training-consistent encode of the training rows reproduces the training ids
+    assert (model.predict(x, reference_quirks=False) == ids).all()
+    # the reference's predict: modulo residuals + unconstrained last layer (raw ids < 2*lc)
+    quirky = model.predict(x)
+    assert (quirky[:, :2] == ids[:, :2]).all() and quirky[:, 2].max() < 32
+    # save / load round trip
+    model.save_model(str(tmp_path / "model"))
+    m2 = HierarchicalRQKMeans(HierarchicalRQKMeansConfig(**SMALL), device=DEV)
+    m2.load_model(str(tmp_path / "model"))
+    assert (m2.predict(x, reference_quirks=False) == ids).all()
+    assert model.get_training_status()["last_completed_layer"] == 2
+    # resume: drop the last layer's checkpoint, retrain only that layer
+    (tmp_path / "ck" / "layer_2_checkpoint.npz").unlink()
+    seeded(43)
+    m3 = HierarchicalRQKMeans(HierarchicalRQKMeansConfig(**SMALL), checkpoint_dir=str(tmp_path / "ck"), device=DEV)
+    r3 = m3.train(x, resume=True)
+    assert (r3["cluster_ids"][0].cpu().numpy() == ids[:, 0]).all()
+    assert (r3["cluster_ids"][1].cpu().numpy() == ids[:, 1]).all()
+
+
+def test_hierarchical_errors():
+    model = HierarchicalRQKMeans(HierarchicalRQKMeansConfig(**SMALL), device=DEV)
+    with pytest.raises(RuntimeError):
+        model.predict(np.zeros((4, 512), np.float32))
+    with pytest.raises(ValueError):
+        model.train(np.zeros((4, 100), np.float32))
+
+
+def test_simplified_train_jsonl(tmp_path):
+    x = synth.small_mixture(1500, m=64, seed=21)
+    sids = [f"s{i:05d}" for i in range(len(x))]
+    csv_path = tmp_path / "vec.csv"
+    rq_io.write_song_vectors(str(csv_path), sids, x)
+    seeded(42)
+    model = SimplifiedHierarchicalRQ(HierarchicalRQKMeansConfig(**SMALL), device=DEV)
+    model.train(str(csv_path))
+    ids = np.array([model.semantic_ids[s] for s in sids])
+    assert ids.shape == (1500, 3) and ids[:, 0].max() < 8 and ids[:, 1].max() < 8 and ids[:, 2].max() < 32
+    out = tmp_path / "ids.jsonl"
+    model.save_semantic_ids(str(out))
+    assert out.read_bytes() == rq_io.semantic_id_lines(sids, ids)
+    model.save_model(str(tmp_path / "m.npz"))
+    m2 = SimplifiedHierarchicalRQ.load_model(str(tmp_path / "m.npz"), device=DEV)
+    assert torch.equal(m2.final_layer_centers.cpu(), model.final_layer_centers.cpu())
