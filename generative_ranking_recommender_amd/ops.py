@@ -305,3 +305,16 @@ def greedy_match(dist: torch.Tensor, sub_off: torch.Tensor, max_take: int):
     _lib.check(lib().rqsid_greedy_match(_ptr(dist), _ptr(sub_off), g, c, int(max_take), _ptr(match), _ptr(nsel),
                                         _stream()), "rqsid_greedy_match")
     return match, nsel[:g]
+
+
+def centroid_sums(x: torch.Tensor, assignment: torch.Tensor, k: int):
+    """Per-cluster fp64 sums and counts of the rows of x (the first half of the Lloyd update; the
+    multi-GPU fit all-reduces these).  Returns (sums f64 [k, D], counts i32 [k])."""
+    _require_device(x)
+    n, d = x.shape
+    b = bucket(assignment, k, rows_per_tile=centroid_tile_rows())
+    sums = torch.zeros((k, d), dtype=torch.float64, device=x.device)
+    _lib.check(lib().rqsid_centroid_accumulate(_ptr(x), d, _ptr(b.row_index), k, _ptr(b.seg_row_off),
+                                               _ptr(b.seg_tile_off), b.max_tiles, _ptr(sums), _stream()),
+               "rqsid_centroid_accumulate")
+    return sums, b.seg_row_off[1:] - b.seg_row_off[:-1]

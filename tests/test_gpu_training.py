@@ -173,3 +173,24 @@ def test_simplified_train_jsonl(tmp_path):
     model.save_model(str(tmp_path / "m.npz"))
     m2 = SimplifiedHierarchicalRQ.load_model(str(tmp_path / "m.npz"), device=DEV)
     assert torch.equal(m2.final_layer_centers.cpu(), model.final_layer_centers.cpu())
+
+
+def test_sharded_lloyd_on_gpu_world1(tmp_path):
+    """The default (GPU kernel) local steps of the row-sharded fit, one rank over RCCL, against the
+    single-process GPU KMeans with the same seeds."""
+    import torch.distributed as dist
+    from generative_ranking_recommender_amd.distributed import ShardedLloyd
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1)
+    try:
+        x = torch.from_numpy(synth.small_mixture(5000, m=20, seed=2)).to(DEV)
+        seeded(3)
+        sl = ShardedLloyd(24, x, len(x))
+        a = sl.fit(iter_limit=5)
+        seeded(3)
+        km = KMeans(n_clusters=24, device=DEV, balanced=False)
+        a_ref = km.fit(x, iter_limit=5)
+        assert (a.cpu() == a_ref).all()
+        torch.testing.assert_close(sl.cluster_centers, km.cluster_centers, rtol=1e-6, atol=1e-6)
+    finally:
+        dist.destroy_process_group()
