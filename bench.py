@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--rows", type=int, default=10_000_000, help="rows per GPU")
-    ap.add_argument("--cpu-sample", type=int, default=200_000, help="rows for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="rows for the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
@@ -173,7 +173,7 @@ def main():
         tfl = n * 2 * keff * D / (t * 1e-3) / 1e12
         kern[f"assign_l{lvl}"] = {"ms": round(t, 3), "GB/s": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
                                   "fp32_equiv_TFLOP/s": round(tfl, 1),
-                                  "bf16x3_mfma_frac": round(3 * tfl / BF16_PEAK_TFLOPS, 4),
+                                  "mfma_f16_frac": round(tfl / BF16_PEAK_TFLOPS, 4),
                                   "rescored_rows": rescored[lvl] if lvl < len(rescored) else None}
     if "residual" in ms:
         t = ms["residual"]

@@ -34,7 +34,7 @@ SIGNATURES = {
     "rqsid_assign_workspace_bytes": (c_i64, [c_i64]),
     "rqsid_assign": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_i64,
                              c_vp, c_vp, c_vp, c_i32,
-                             c_vp, c_vp, c_i32, c_vp, c_vp,
+                             c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
                              c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_vp, c_vp, c_vp, c_i64, c_vp]),
     "rqsid_residual": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),

@@ -36,6 +36,8 @@ namespace rqsid {
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(2))) _Float16 h2;
+typedef __attribute__((ext_vector_type(2))) float f2;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 constexpr int kWaves = 4;
@@ -71,6 +73,7 @@ struct AssignParams {
   const int32_t* cand_base;
   const int32_t* cand_count;
   const int32_t* cand_idx;
+  const int32_t* cand_lid;  // local id reported for list position j (NULL: j)
   const uint8_t* seg_flags;
   int32_t* out_local;
   int32_t* out_global;
@@ -88,6 +91,9 @@ struct AssignParams {
 
 __device__ __forceinline__ int cand_global(const AssignParams& p, int base, int local) {
   return p.cand_idx ? p.cand_idx[base + local] : base + local;
+}
+__device__ __forceinline__ int cand_local(const AssignParams& p, int base, int pos) {
+  return p.cand_lid ? p.cand_lid[base + pos] : pos;
 }
 __device__ __forceinline__ int seg_row(const int32_t* map, int s) { return map ? map[s] : s; }
 
@@ -156,8 +162,11 @@ __device__ __forceinline__ void wait_barrier() {
 
 template <int S, int P>
 __device__ __forceinline__ void wait_chunks(int younger) {
-  // younger = chunks issued after the one we need (uniform); each chunk is P DMA ops per wave
-  if (S >= 5 && younger >= 3) wait_barrier<(S >= 5 ? 3 * P : 0)>();
+  // younger = chunks issued after the one we need (uniform, <= S-2); each chunk is P DMA ops per wave
+  static_assert((S - 2) * P <= 63, "vmcnt field is 6 bits");
+  if (S >= 7 && younger >= 5) wait_barrier<(S >= 7 ? 5 * P : 0)>();
+  else if (S >= 6 && younger >= 4) wait_barrier<(S >= 6 ? 4 * P : 0)>();
+  else if (S >= 5 && younger >= 3) wait_barrier<(S >= 5 ? 3 * P : 0)>();
   else if (S >= 4 && younger >= 2) wait_barrier<(S >= 4 ? 2 * P : 0)>();
   else if (younger >= 1) wait_barrier<P>();
   else wait_barrier<0>();
@@ -170,8 +179,8 @@ template <int NT, int S>
 struct ScreenLayout {
   static constexpr int kCStage = NT * 32 * 64;  // NT*32 candidates x 32 fp16 dims
   static constexpr int kStage = kXStage + kCStage;
-  static constexpr int kMeta = S * kStage;       // float2 {|c|^2, |c|} per candidate of the pass
-  static constexpr int kRatio = kMeta + NT * 32 * 8;
+  static constexpr int kMeta = S * kStage;       // float4 {|c|^2, |c|, e0, 0} per candidate of the pass
+  static constexpr int kRatio = kMeta + NT * 32 * 16;
   static constexpr int kRes = kRatio + 16;        // residual rows ca, cb (fp32, dim each)
   static constexpr int bytes(int rl, int dim) { return kRes + rl * dim * 4; }
   static constexpr int kMaxBytes = kRes + 2 * kMaxDim * 4;
@@ -201,7 +210,7 @@ __device__ __forceinline__ void push_work(const AssignParams& p, bool need, int 
 inline float accumulation_rel(int dim) { return (float)(((dim / 16) * 17.0 + 8.0) * std::ldexp(1.0, -23) * 1.02); }
 
 template <int NT, int S, int RL, bool NORM>
-__global__ __launch_bounds__(256, NT == 4 ? 2 : 1) void assign_screen_kernel(AssignParams p) {
+__global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <= 3) ? 2 : 1)) void assign_screen_kernel(AssignParams p) {
   using L = ScreenLayout<NT, S>;
   constexpr int P = 4 + NT / 2;  // DMA ops per wave per chunk (x: 4, centres: NT/2)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -278,9 +287,9 @@ __global__ __launch_bounds__(256, NT == 4 ? 2 : 1) void assign_screen_kernel(Ass
     llb[j] = INFINITY;
   }
   double sv2 = 0.0;            // sum v^2 in fp64 (NORM: the normalising denominator is exact)
-  float sf2 = 0.f, se2 = 0.f;  // sum v^2 (fp32, bound only), sum (v - fp16(v))^2
+  f2 sf2v = {0.f, 0.f}, se2v = {0.f, 0.f};  // sum v^2 (fp32, bound only), sum (v - fp16(v))^2
   float vn = 0.f, en = 0.f, inv_den = 1.f, dr = 0.f;
-  float2* lds_meta = reinterpret_cast<float2*>(smem + L::kMeta);
+  float4* lds_meta = reinterpret_cast<float4*>(smem + L::kMeta);
   unsigned* lds_ratio = reinterpret_cast<unsigned*>(smem + L::kRatio);
   const f32x16 zero16 = {};
   const int xsw = (r >> 1) & 7;  // swizzle of this lane's row in the x image
@@ -302,9 +311,11 @@ __global__ __launch_bounds__(256, NT == 4 ? 2 : 1) void assign_screen_kernel(Ass
     if (tid < 2) lds_ratio[tid] = 0u;
     __syncthreads();
     if (tid < NT * 32) {
-      const int kl = pbase + tid < cnt ? pbase + tid : cnt - 1;
+      const bool live = pbase + tid < cnt;
+      const int kl = live ? pbase + tid : cnt - 1;
       const float4 m = reinterpret_cast<const float4*>(p.c_meta)[cand_global(p, cbase, kl)];
-      lds_meta[tid] = make_float2(m.x, m.y);
+      // {|c|^2, |c|, e0 = the fp32 epilogue's own rounding allowance}; padding candidates get |c|^2 = inf
+      lds_meta[tid] = make_float4(live ? m.x : INFINITY, m.y, fmaf(2.39e-7f, m.x, 1e-30f), 0.f);
       // positive floats order like their bit patterns
       atomicMax(&lds_ratio[0], __float_as_uint(m.y > 0.f ? m.z / m.y * 1.000001f : (m.z > 0.f ? INFINITY : 0.f)));
     }
@@ -333,32 +344,43 @@ __global__ __launch_bounds__(256, NT == 4 ? 2 : 1) void assign_screen_kernel(Ass
         const int q0 = 4 * ks + 2 * h;
         const float4 xa = *reinterpret_cast<const float4*>(xb + ((q0 ^ xsw) << 4));
         const float4 xc = *reinterpret_cast<const float4*>(xb + (((q0 + 1) ^ xsw) << 4));
-        float v[8] = {xa.x, xa.y, xa.z, xa.w, xc.x, xc.y, xc.z, xc.w};
+        // packed fp32 pairs: every VALU op below handles two elements (v_pk_*), the fp16 conversion
+        // is v_cvt_pk_f16_f32 (round to nearest even).  fp16 inputs keep denormals (hipcc's default
+        // MODE; pinned by tests/test_mfma_numerics.py::test_f16_denormals_are_kept) and an input
+        // beyond the fp16 range becomes inf, which makes the row's bound infinite -> exact re-score.
+        f2 v[4] = {f2{xa.x, xa.y}, f2{xa.z, xa.w}, f2{xc.x, xc.y}, f2{xc.z, xc.w}};
         const int d0 = c * kChunk + 16 * ks + 8 * h;
         if (RL >= 1) {
           const float4 a0 = *reinterpret_cast<const float4*>(lds_ca + d0);
           const float4 a1 = *reinterpret_cast<const float4*>(lds_ca + d0 + 4);
-          const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+          const f2 av[4] = {f2{a0.x, a0.y}, f2{a0.z, a0.w}, f2{a1.x, a1.y}, f2{a1.z, a1.w}};
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = v[e] - av[e];  // exact fp32, as the reference
+          for (int e = 0; e < 4; ++e) v[e] = v[e] - av[e];  // exact fp32, as the reference
         }
         if (RL >= 2) {
           const float4 b0 = *reinterpret_cast<const float4*>(lds_cb + d0);
           const float4 b1v = *reinterpret_cast<const float4*>(lds_cb + d0 + 4);
-          const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1v.x, b1v.y, b1v.z, b1v.w};
+          const f2 bv[4] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1v.x, b1v.y}, f2{b1v.z, b1v.w}};
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = (NORM ? v[e] * inv1 : v[e]) - bv[e];
+          for (int e = 0; e < 4; ++e) v[e] = (NORM ? v[e] * inv1 : v[e]) - bv[e];
         }
-        f16x8 bf;
+        h2 hh[4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const _Float16 hv = to_f16(v[e]);
-          bf[e] = hv;
-          if (pass == 0) {
-            const float ex = v[e] - (float)hv;  // exact: the fp16 rounding residual
-            se2 = fmaf(ex, ex, se2);
-            if (NORM && RL >= 1) sv2 = fma((double)v[e], (double)v[e], sv2);
-            else sf2 = fmaf(v[e], v[e], sf2);
+        for (int e = 0; e < 4; ++e) hh[e] = __builtin_convertvector(v[e], h2);
+        const f16x8 bf = __builtin_shufflevector(__builtin_shufflevector(hh[0], hh[1], 0, 1, 2, 3),
+                                                 __builtin_shufflevector(hh[2], hh[3], 0, 1, 2, 3),
+                                                 0, 1, 2, 3, 4, 5, 6, 7);
+        if (pass == 0) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const f2 ex = v[e] - __builtin_convertvector(hh[e], f2);  // exact: the fp16 rounding residual
+            se2v = ex * ex + se2v;
+            if (NORM && RL >= 1) {
+              sv2 = fma((double)v[e].x, (double)v[e].x, sv2);
+              sv2 = fma((double)v[e].y, (double)v[e].y, sv2);
+            } else {
+              sf2v = v[e] * v[e] + sf2v;
+            }
           }
         }
         const int qa = (2 * ks + h) ^ csw;
@@ -381,6 +403,7 @@ __global__ __launch_bounds__(256, NT == 4 ? 2 : 1) void assign_screen_kernel(Ass
     }
 
     if (pass == 0) {
+      const float se2 = se2v.x + se2v.y, sf2 = sf2v.x + sf2v.y;
       const float e2 = se2 + __shfl_xor(se2, 32);
       en = sqrtf(e2) * 1.001f + 1e-30f;
       float nrm;
@@ -407,29 +430,32 @@ __global__ __launch_bounds__(256, NT == 4 ? 2 : 1) void assign_screen_kernel(Ass
     const float K = 2.0f * inv_den * 1.000001f * (en + hn * rho + p.acc_rel * hn * (1.0f + rho)) + 2.0f * dr +
                     4.8e-7f * vr;
     const float m2 = -2.0f * inv_den;
-    const float2* meta = lds_meta + 4 * h;
+    const float4* meta = lds_meta + 4 * h;
     const int kl_h = pbase + 4 * h;
+    // sweep 1: U = least upper bound.  The scheduling barriers stop hipcc from hoisting every
+    // tile's meta reads at once (256 VGPRs -> spills at 2 waves/SIMD).
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int io = t * 32 + (v & 3) + 8 * (v >> 2);
-        const float2 m = meta[io];  // |c|^2, |c|
+        const float4 m = meta[io];  // |c|^2 (inf for padding), |c|, e0
         const float sc = fmaf(m2, acc[t][v], m.x);
-        const float e = fmaf(K, m.y, fmaf(2.39e-7f, m.x, 1e-30f));
-        U = fminf(U, kl_h + io < cnt ? sc + e : INFINITY);
+        U = fminf(U, sc + fmaf(K, m.y, m.z));
       }
     }
     U = fminf(U, __shfl_xor(U, 32));
+    // sweep 2: list the candidates whose lower bound (recomputed) is <= U, ascending
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-        const int io = t * 32 + (v & 3) + 8 * (v >> 2);
-        const int kl = kl_h + io;
-        const float2 m = meta[io];
-        const float lb = fmaf(m2, acc[t][v], m.x) - fmaf(K, m.y, fmaf(2.39e-7f, m.x, 1e-30f));
-        const bool q = kl < cnt && lb <= U;
+        const int kl = kl_h + t * 32 + (v & 3) + 8 * (v >> 2);
+        const float4 m = meta[t * 32 + (v & 3) + 8 * (v >> 2)];
+        const float lb = fmaf(m2, acc[t][v], m.x) - fmaf(K, m.y, m.z);
+        const bool q = lb <= U && kl < cnt;
         if (__builtin_amdgcn_ballot_w64(q)) {  // wave-uniform skip: most candidates qualify for no row
 #pragma unroll
           for (int j = 0; j < kListPerHalf; ++j) {
@@ -467,7 +493,7 @@ __global__ __launch_bounds__(256, NT == 4 ? 2 : 1) void assign_screen_kernel(Ass
     int k = -1;
 #pragma unroll
     for (int j = 0; j < kListPerHalf; ++j) k = max(k, max(kk[j], kp[j]));
-    p.out_local[my_row] = k;
+    p.out_local[my_row] = cand_local(p, cbase, k);
     p.out_global[my_row] = cand_global(p, cbase, k);
   }
   WorkItem w{};
@@ -518,6 +544,8 @@ __global__ __launch_bounds__(256) void assign_rescore_kernel(AssignParams p) {
   const int64_t nitems_raw = *p.work_count;
   const int64_t nitems = nitems_raw < p.work_cap ? nitems_raw : p.work_cap;
   const int nv = p.dim / 4;
+  // Items are strided over every wave of the grid: the "every candidate" rows cluster in a few
+  // segments (duplicated centres), and striding spreads them evenly over the waves.
   for (int64_t it = wid; it < nitems; it += nw) {
     const WorkItem w = p.work[it];
     const float* xr = p.x + (int64_t)w.row * p.dim;
@@ -641,7 +669,7 @@ __global__ __launch_bounds__(256) void assign_rescore_kernel(AssignParams p) {
     }
     if (lane == 0) {
       const bool found = bj != INT_MAX;
-      p.out_local[w.row] = found && !penalty ? bj : -1;
+      p.out_local[w.row] = found && !penalty ? cand_local(p, base, bj) : -1;
       p.out_global[w.row] = found ? (penalty ? bj : cand_global(p, base, bj)) : -1;
     }
   }
@@ -696,12 +724,25 @@ void set_attrs(bool* ok) {
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) *ok = false;
 }
 
+// ring-depth variant (tuning experiments): 0 (default) S=2; 1: NT4 S6 / NT8 S3; 3: NT4 S3 / NT8 S4
+int screen_variant() {
+  static int v = [] {
+    const char* e = getenv("RQSID_SCREEN_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 bool g_attr_done = false;
 int ensure_attrs() {
   if (g_attr_done) return RQSID_OK;
   bool ok = true;
   set_attrs<4, 3>(&ok);
+  set_attrs<4, 6>(&ok);
   set_attrs<8, 4>(&ok);
+  set_attrs<8, 3>(&ok);
+  set_attrs<4, 2>(&ok);
+  set_attrs<8, 2>(&ok);
   if (!ok) return fail(RQSID_E_LAUNCH, "assign: cannot raise the dynamic LDS limit");
   g_attr_done = true;
   return RQSID_OK;
@@ -744,7 +785,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
                  const int32_t* seg_row_off, const int32_t* seg_tile_off, int64_t max_tiles, const float* centers,
                  const uint16_t* c16, const float* c_meta, int32_t n_centers, const int32_t* cand_base,
                  const int32_t* cand_count, int32_t cand_count_max, const int32_t* cand_idx,
-                 const uint8_t* seg_flags, int32_t res_levels, int32_t res_normalize, const float* ca,
+                 const int32_t* cand_lid, const uint8_t* seg_flags, int32_t res_levels, int32_t res_normalize, const float* ca,
                  const int32_t* seg_ca, const float* cb, const int32_t* seg_cb, const float* den_in,
                  float* den_out, int32_t* out_local, int32_t* out_global, void* workspace,
                  int64_t workspace_bytes, void* stream) {
@@ -777,6 +818,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   p.cand_base = cand_base;
   p.cand_count = cand_count;
   p.cand_idx = cand_idx;
+  p.cand_lid = cand_lid;
   p.seg_flags = seg_flags;
   p.out_local = out_local;
   p.out_global = out_global;
@@ -793,10 +835,21 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   const bool norm = res_normalize != 0;
   if (hipMemsetAsync(workspace, 0, 256, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "assign: memset");
   const unsigned grid = (unsigned)((max_tiles + 7) / 8 * 8);  // XCD remap needs a multiple of 8
-  if (cand_count_max <= 128) launch_screen<4, 3>(p, res_levels, norm, grid, st);
-  else launch_screen<8, 4>(p, res_levels, norm, grid, st);
+  // Measured on MI355X (tools/screen_sweep.py): independent blocks per CU beat ring depth: NT4 with
+  // S=2 runs 3 blocks/CU, NT8 with S=2 runs 2 blocks/CU (RQSID_SCREEN_VARIANT=1/3 select the older
+  // deeper-ring single-block configurations for comparison).
+  const int v = screen_variant();
+  if (cand_count_max <= 128) {
+    if (v == 1) launch_screen<4, 6>(p, res_levels, norm, grid, st);
+    else if (v == 3) launch_screen<4, 3>(p, res_levels, norm, grid, st);
+    else launch_screen<4, 2>(p, res_levels, norm, grid, st);
+  } else {
+    if (v == 1) launch_screen<8, 3>(p, res_levels, norm, grid, st);
+    else if (v == 3) launch_screen<8, 4>(p, res_levels, norm, grid, st);
+    else launch_screen<8, 2>(p, res_levels, norm, grid, st);
+  }
   if ((rc = check_launch("assign_screen"))) return rc;
-  const dim3 g(grid_cap(cdiv(n_rows, 4), 4096));
+  const dim3 g(4096);  // multiple of 8 (XCD-grouped work runs)
   if (res_levels == 0) hipLaunchKernelGGL((assign_rescore_kernel<0, false>), g, dim3(256), 0, st, p);
   else if (res_levels == 1 && norm) hipLaunchKernelGGL((assign_rescore_kernel<1, true>), g, dim3(256), 0, st, p);
   else if (res_levels == 1) hipLaunchKernelGGL((assign_rescore_kernel<1, false>), g, dim3(256), 0, st, p);

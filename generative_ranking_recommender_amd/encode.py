@@ -69,22 +69,22 @@ class RQEncoder:
         self.has_penalty = False
         for l in range(self.L):
             if l == 0:
-                self.cands.append(ops.Candidates(torch.zeros(1, dtype=torch.int32, device=device),
-                                                 torch.full((1,), self.pcs[0].k, dtype=torch.int32, device=device),
-                                                 self.pcs[0].k))
+                c = ops.Candidates(torch.zeros(1, dtype=torch.int32, device=device),
+                                   torch.full((1,), self.pcs[0].k, dtype=torch.int32, device=device), self.pcs[0].k)
             elif l < self.L - 1:
-                self.cands.append(ops.contiguous_candidates(self.need[l - 1], self.need[l], device))
+                c = ops.contiguous_candidates(self.need[l - 1], self.need[l], device)
             else:
                 if match is not None and semantics.match_lookup:
                     m = match.to(device)
                     c = ops.match_to_candidates(m)
                     self.has_penalty = bool((c.count == 0).any().item())
                     self.n_groups = m.shape[0]
-                    self.cands.append(c)
                 else:
                     k = self.pcs[l].k
-                    self.cands.append(ops.Candidates(torch.zeros(1, dtype=torch.int32, device=device),
-                                                     torch.full((1,), k, dtype=torch.int32, device=device), k))
+                    c = ops.Candidates(torch.zeros(1, dtype=torch.int32, device=device),
+                                       torch.full((1,), k, dtype=torch.int32, device=device), k)
+            # bitwise-duplicate centres can never be the first minimum: drop them from the lists
+            self.cands.append(ops.dedup_candidates(c, self.pcs[l].centers))
         self._ws = None
         self.last_rescored = []
         self.force_materialized = False

@@ -114,6 +114,7 @@ class Candidates:
     count_max: int
     idx: Optional[torch.Tensor] = None   # i32
     flags: Optional[torch.Tensor] = None  # u8 [S]
+    lid: Optional[torch.Tensor] = None   # i32: local id reported for list position (None: the position)
 
 
 def contiguous_candidates(n_segments: int, per_segment: int, device) -> Candidates:
@@ -138,6 +139,40 @@ def match_to_candidates(match: torch.Tensor) -> Candidates:
     # the maximum allowed count decides the kernel variant; match rows are host-known data
     cmax = int(match.sum(1).max().item()) if g else 0
     return Candidates(base, cnt, cmax, idx, flags)
+
+
+def dedup_candidates(cand: Candidates, centers: torch.Tensor) -> Candidates:
+    """Drop every list entry whose centre is bitwise identical to an EARLIER entry of the same list.
+
+    Exact: identical centres have identical distances, and the reference's argmin returns the first
+    of equal minima, so a later duplicate can never be the answer.  The kept entries report their
+    original local ids through ``lid``.  Without duplicates the input is returned unchanged."""
+    dev = centers.device
+    canon = torch.unique(centers.float().contiguous().view(torch.int32), dim=0, return_inverse=True)[1]
+    n_unique = int(canon.max().item()) + 1 if centers.shape[0] else 0
+    if n_unique == centers.shape[0]:
+        return cand  # no duplicate rows at all
+    S = cand.base.numel()
+    cnt = cand.count.long()
+    total = int(cnt.sum().item())
+    seg = torch.repeat_interleave(torch.arange(S, device=dev), cnt)
+    off = torch.zeros(S + 1, dtype=torch.long, device=dev)
+    off[1:] = torch.cumsum(cnt, 0)
+    pos = torch.arange(total, device=dev) - off[seg]
+    if cand.idx is None:
+        glob = cand.base.long()[seg] + pos
+    else:
+        glob = cand.idx.long()[cand.base.long()[seg] + pos]
+    lid_in = pos if cand.lid is None else cand.lid.long()[cand.base.long()[seg] + pos]
+    key = seg * n_unique + canon[glob]
+    first = torch.full((int(key.max().item()) + 1,), total, dtype=torch.long, device=dev)
+    first.scatter_reduce_(0, key, pos + off[seg], reduce="amin")
+    keep = first[key] == pos + off[seg]
+    new_cnt = torch.zeros(S, dtype=torch.long, device=dev).index_add_(0, seg, keep.long())
+    new_base = torch.zeros(S, dtype=torch.long, device=dev)
+    new_base[1:] = torch.cumsum(new_cnt, 0)[:-1]
+    return Candidates(new_base.to(torch.int32), new_cnt.to(torch.int32), int(new_cnt.max().item()) if S else 0,
+                      glob[keep].to(torch.int32).contiguous(), cand.flags, lid_in[keep].to(torch.int32).contiguous())
 
 
 class AssignWorkspace:
@@ -193,7 +228,7 @@ def assign(x: torch.Tensor, pc: PreparedCenters, buckets: Buckets, cand: Candida
         _ptr(x), n, d, _ptr(buckets.row_index), buckets.n_segments, _ptr(buckets.seg_row_off),
         _ptr(buckets.seg_tile_off), buckets.max_tiles,
         _ptr(pc.centers), _ptr(pc.c16), _ptr(pc.meta), pc.k,
-        _ptr(cand.base), _ptr(cand.count), cand.count_max, _ptr(cand.idx), _ptr(cand.flags),
+        _ptr(cand.base), _ptr(cand.count), cand.count_max, _ptr(cand.idx), _ptr(cand.lid), _ptr(cand.flags),
         0 if f is None else f.levels, 0 if f is None else int(f.normalize),
         None if f is None else _ptr(f.ca), None if f is None else _ptr(f.seg_ca),
         None if f is None else _ptr(f.cb), None if f is None else _ptr(f.seg_cb),

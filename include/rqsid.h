@@ -65,8 +65,10 @@ int32_t rqsid_assign_tile_rows(void);
  * Segment s owns rows row_index[seg_row_off[s] .. seg_row_off[s+1]) (row_index
  * NULL = identity) and candidates j = 0 .. cand_count[s]-1 whose global centre
  * index is cand_idx[cand_base[s]+j] (cand_idx NULL: cand_base[s]+j).
- * out_local[row] = j of the nearest allowed centre, out_global[row] = its global
- * index.  Segments flagged RQSID_SEG_PENALTY reproduce the reference's +10000
+ * out_local[row] = cand_lid[cand_base[s]+j] (cand_lid NULL: j) of the nearest allowed
+ * centre, out_global[row] = its global index.  (A list may omit bitwise duplicates of an
+ * earlier entry -- they can never be the first minimum -- and report the original local
+ * ids through cand_lid.)  Segments flagged RQSID_SEG_PENALTY reproduce the reference's +10000
  * mask with an empty allowed set (argmin over all n_centers of fl32(d)+10000);
  * their out_local is -1.
  *
@@ -95,7 +97,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
                  const float* centers, const uint16_t* c16, const float* c_meta,
                  int32_t n_centers,
                  const int32_t* cand_base, const int32_t* cand_count, int32_t cand_count_max,
-                 const int32_t* cand_idx, const uint8_t* seg_flags,
+                 const int32_t* cand_idx, const int32_t* cand_lid, const uint8_t* seg_flags,
                  int32_t res_levels, int32_t res_normalize,
                  const float* ca, const int32_t* seg_ca, const float* cb, const int32_t* seg_cb,
                  const float* den_in, float* den_out,

@@ -83,3 +83,18 @@ def test_block_sum_rounding_model(f16):
     scale = {"cancel": 2.0 ** 26, "big_plus_ones": 2.0 ** 26, "tiny_plus_one": 2.0, "c_plus_14": 2.0 ** 26}
     for k, v in res.items():
         assert abs(v - exact[k]) <= 17 * 2.0 ** -23 * scale[k], (k, v)
+
+
+def test_f16_denormals_are_kept():
+    """The fp16 screen feeds denormal fp16 values to v_mfma_f32_32x32x16_f16 and relies on them being
+    used exactly (no flush to zero), as hipcc's default FP16 denormal mode promises."""
+    a = np.zeros((32, 16), np.float32)
+    b = np.zeros((16, 32), np.float32)
+    a[0, 0], b[0, 0] = 2.0 ** -20, 2.0 ** 10     # denormal x normal
+    a[1, 0], b[0, 1] = 2.0 ** -24, 0.0
+    a[1, 1], b[1, 1] = 2.0 ** -24, 2.0 ** -24     # smallest denormal squared (fp32 normal)
+    a[2, 2], b[2, 2] = 2.0 ** -15 + 2.0 ** -24, 2.0 ** 3
+    d = probe(a, b, np.zeros((32, 32), np.float32), f16=True)
+    assert d[0, 0] == 2.0 ** -10
+    assert d[1, 1] == 2.0 ** -48
+    assert d[2, 2] == (2.0 ** -15 + 2.0 ** -24) * 8
