@@ -117,7 +117,8 @@ class RQEncoder:
         return True
 
     def encode(self, x: torch.Tensor, count_rescored: bool = False) -> torch.Tensor:
-        """x: f32 [N, D] on the device -> int32 [N, L] semantic IDs."""
+        """x: f32 [N, D] on the device -> int32 [N, L] semantic IDs (a transposed view of the
+        level-major [L, N] buffer the kernels write; no copy)."""
         if x.dim() != 2 or x.shape[1] != self.dim:
             raise ValueError(f"Input dimension {x.shape[-1]} does not match config embedding_dim {self.dim}")
         x = x.float().contiguous()
@@ -131,7 +132,7 @@ class RQEncoder:
             self._encode_fused(x, out, ws, count_rescored)
         else:
             self._encode_materialized(x, out, ws, count_rescored)
-        return out.t().contiguous()
+        return out.t()
 
     def _last_level_buckets(self, out, l, n, device):
         if self.sem.match_lookup:
@@ -156,10 +157,9 @@ class RQEncoder:
         n = x.shape[0]
         dev = x.device
         norm = self.sem.normalize_residual
-        glob0 = torch.empty(n, dtype=torch.int32, device=dev)
-        ops.assign(x, self.pcs[0], ops.single_segment(n, dev), self.cands[0], out_local=out[0], out_global=glob0,
+        # level 0 is one segment over every centre: the local id IS the global id
+        ops.assign(x, self.pcs[0], ops.single_segment(n, dev), self.cands[0], out_local=out[0], out_global=out[0],
                    workspace=ws)
-        out[0].copy_(glob0)
         if count_rescored:
             self.last_rescored.append(ws.rescored())
         if self.L == 1:
