@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--rows", type=int, default=10_000_000, help="rows per GPU")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="rows for the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--codebooks", choices=("fitted", "sampled"), default=os.environ.get("BENCH_CODEBOOKS", "fitted"),
+                    help="fitted: short K-Means fits on a sample (trained-model geometry); sampled: residual rows")
     return ap.parse_args()
 
 
@@ -86,6 +88,65 @@ def make_rows(n, rank, device):
     return x
 
 
+def _lloyd(x, k, iters, gen):
+    """Short unbalanced K-Means on the device (rqsid nearest + fp64 centroid sums); empty clusters
+    keep their previous centre.  Initial centres: k distinct rows (with replacement when k > n)."""
+    n = x.shape[0]
+    if n >= k:
+        init = torch.randperm(n, device=x.device, generator=gen)[:k]
+    else:
+        init = torch.randint(0, n, (k,), device=x.device, generator=gen)
+    c = x[init].clone()
+    for _ in range(iters):
+        a = ops.nearest(x, ops.prepare_centers(c))
+        c, _ = ops.centroid_update(x, a, k, c)
+    return c
+
+
+def fitted_codebooks(device, n_sample=1_000_000, seed=4321, iters=10):
+    """PROD-shaped codebooks FITTED on a sample of the bench distribution (what a trained model's
+    codebooks look like): C1 = K-Means(128) of the rows; C2 = per-parent K-Means(128) of the
+    normalised level-1 residuals; C3 = K-Means(2560) of the normalised level-2 residuals; match row
+    of an (l1,l2) group = the 256 candidates nearest the mean residual of the group's sample rows
+    (random columns for groups with no sample rows).  Short Lloyd fits (``iters`` iterations,
+    unbalanced): the geometry of trained centroids, not the reference's balanced training."""
+    gen = torch.Generator(device=device).manual_seed(seed)
+    x = make_rows(n_sample, 10_000 + seed, device)
+    c0 = _lloyd(x, NEED[0], iters, gen)
+    a0 = ops.nearest(x, ops.prepare_centers(c0))
+    r1 = ops.residual(x, c0, a0, normalize=True)
+    order = torch.argsort(a0, stable=True)
+    cnt0 = torch.bincount(a0.long(), minlength=NEED[0]).cpu().tolist()
+    c1 = torch.empty((NEED[0] * NEED[1], D), dtype=torch.float32, device=device)
+    a1 = torch.empty(n_sample, dtype=torch.int32, device=device)
+    start = 0
+    for p in range(NEED[0]):
+        rows = order[start:start + cnt0[p]]
+        start += cnt0[p]
+        sub = r1[rows] if len(rows) else r1[:1]
+        cp = _lloyd(sub, NEED[1], iters, gen)
+        c1[p * NEED[1]:(p + 1) * NEED[1]] = cp
+        if len(rows):
+            a1[rows] = ops.nearest(sub, ops.prepare_centers(cp)) + p * NEED[1]
+    r2 = ops.residual(r1, c1, a1, normalize=True)
+    c2 = _lloyd(r2, N_CAND, iters, gen)
+    groups = NEED[0] * NEED[1]
+    sums = torch.zeros((groups, D), dtype=torch.float32, device=device).index_add_(0, a1.long(), r2)
+    cnt = torch.bincount(a1.long(), minlength=groups)
+    means = sums / cnt.clamp(min=1).unsqueeze(1).float()
+    near = torch.topk(ops.pairwise_distance(means.contiguous(), c2), NEED[2], dim=1, largest=False).indices
+    rand = torch.argsort(torch.rand((groups, N_CAND), device=device, generator=gen), dim=1)[:, :NEED[2]]
+    cols = torch.where((cnt > 0).unsqueeze(1), near, rand)
+    match = torch.zeros((groups, N_CAND), dtype=torch.uint8, device=device).scatter_(1, cols, 1)
+    return {"c0": c0.cpu().numpy(), "c1": c1.cpu().numpy(), "c2": c2.cpu().numpy(), "match": match.cpu().numpy()}
+
+
+def codebooks(kind, device):
+    if kind == "fitted":
+        return fitted_codebooks(device)
+    return synth.encode_codebooks(seed=99)
+
+
 def cpu_baseline(cb, rows):
     from threadpoolctl import threadpool_info
     from oracle import rq_oracle as O
@@ -113,7 +174,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    cb = synth.encode_codebooks(seed=99)
+    cb = codebooks(args.codebooks, dev)
     enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], NEED, match=torch.from_numpy(cb["match"]),
                     semantics=HIERARCHICAL_TRAIN, device=dev)
     n = args.rows

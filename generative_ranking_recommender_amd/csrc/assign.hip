@@ -97,11 +97,13 @@ __device__ __forceinline__ int cand_local(const AssignParams& p, int base, int p
 }
 __device__ __forceinline__ int seg_row(const int32_t* map, int s) { return map ? map[s] : s; }
 
-// fp16 operand with a rigorous residual: values outside the fp16 NORMAL range go in as 0 (their whole
-// value then lands in the measured residual), so the bound never depends on denormal/overflow handling.
+// fp16 centre operand with a rigorous residual: round to nearest, keeping fp16 denormals (the MFMA uses
+// them exactly: tests/test_mfma_numerics.py::test_f16_denormals_are_kept, the same mode the row side
+// relies on); values beyond the fp16 range go in as 0, so their whole value lands in |c - c16|.
+// Zeroing small values instead would inflate |c - c16| of a small-norm centroid (a K-Means mean of
+// noise-like residuals) many times over.
 __device__ __forceinline__ _Float16 to_f16(float v) {
-  const float a = fabsf(v);
-  return (_Float16)((a >= 0x1p-14f && a < 65504.0f) ? v : 0.0f);
+  return (_Float16)(fabsf(v) < 65504.0f ? v : 0.0f);
 }
 
 // ---------------------------------------------------------------------------
@@ -180,8 +182,7 @@ struct ScreenLayout {
   static constexpr int kCStage = NT * 32 * 64;  // NT*32 candidates x 32 fp16 dims
   static constexpr int kStage = kXStage + kCStage;
   static constexpr int kMeta = S * kStage;       // float4 {|c|^2, |c|, e0, 0} per candidate of the pass
-  static constexpr int kRatio = kMeta + NT * 32 * 16;
-  static constexpr int kRes = kRatio + 16;        // residual rows ca, cb (fp32, dim each)
+  static constexpr int kRes = kMeta + NT * 32 * 16;        // residual rows ca, cb (fp32, dim each)
   static constexpr int bytes(int rl, int dim) { return kRes + rl * dim * 4; }
   static constexpr int kMaxBytes = kRes + 2 * kMaxDim * 4;
 };
@@ -204,9 +205,11 @@ __device__ __forceinline__ void push_work(const AssignParams& p, bool need, int 
 //   |v.c - vh.ch| <= |ex||c| + |vh||ec|                       (Cauchy-Schwarz, exact norms)
 //   MFMA accumulation <= acc_rel * |vh||ch|                    (tests/test_mfma_numerics.py: each
 //      v_mfma_f32_32x32x16_f16 charged 17 truncating additions at 1 ulp of |C| + sum|products|)
-// so d^2 = |c|^2 - 2 v.c/den is known to within e_k = K |c_k| + 2^-22 |c_k|^2 with the per-row
-//   K = 2/den (|ex| + |vh| rho + acc_rel |vh| (1 + rho)) + 2 dr + 2^-21 |r|
-// (rho = the pass's largest |ec_k|/|c_k|, dr = the rounding of the reference's r = v/den).
+// so d^2 = |c|^2 - 2 v.c/den is known to within e_k = A |c_k| + B |ec_k| + 2^-22 |c_k|^2 with the per-row
+//   A = 2/den (|ex| + acc_rel |vh|) + 2 dr + 2^-21 |r|,   B = 2/den |vh| (1 + acc_rel)
+// (|ch_k| <= |c_k| + |ec_k|; dr = the rounding of the reference's r = v/den).  The centre term is per
+// candidate: a near-zero centroid (large RELATIVE fp16 error, tiny absolute error) loosens only its own
+// bound.
 inline float accumulation_rel(int dim) { return (float)(((dim / 16) * 17.0 + 8.0) * std::ldexp(1.0, -23) * 1.02); }
 
 template <int NT, int S, int RL, bool NORM>
@@ -290,7 +293,6 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
   f2 sf2v = {0.f, 0.f}, se2v = {0.f, 0.f};  // sum v^2 (fp32, bound only), sum (v - fp16(v))^2
   float vn = 0.f, en = 0.f, inv_den = 1.f, dr = 0.f;
   float4* lds_meta = reinterpret_cast<float4*>(smem + L::kMeta);
-  unsigned* lds_ratio = reinterpret_cast<unsigned*>(smem + L::kRatio);
   const f32x16 zero16 = {};
   const int xsw = (r >> 1) & 7;  // swizzle of this lane's row in the x image
   const int csw = (r >> 2) & 3;  // swizzle of this lane's candidate row in the centre image
@@ -308,16 +310,14 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
       const int slot = (lane & 3) ^ ((il >> 2) & 3);
       csrc[j] = reinterpret_cast<const _Float16*>(p.c16) + (int64_t)cg * dim + slot * 8;
     }
-    if (tid < 2) lds_ratio[tid] = 0u;
     __syncthreads();
     if (tid < NT * 32) {
       const bool live = pbase + tid < cnt;
       const int kl = live ? pbase + tid : cnt - 1;
       const float4 m = reinterpret_cast<const float4*>(p.c_meta)[cand_global(p, cbase, kl)];
-      // {|c|^2, |c|, e0 = the fp32 epilogue's own rounding allowance}; padding candidates get |c|^2 = inf
-      lds_meta[tid] = make_float4(live ? m.x : INFINITY, m.y, fmaf(2.39e-7f, m.x, 1e-30f), 0.f);
-      // positive floats order like their bit patterns
-      atomicMax(&lds_ratio[0], __float_as_uint(m.y > 0.f ? m.z / m.y * 1.000001f : (m.z > 0.f ? INFINITY : 0.f)));
+      // {|c|^2, |c|, e0 = the fp32 epilogue's own rounding allowance, |c - c16|}; padding candidates
+      // get |c|^2 = inf
+      lds_meta[tid] = make_float4(live ? m.x : INFINITY, m.y, fmaf(2.39e-7f, m.x, 1e-30f), m.z);
     }
 #pragma unroll
     for (int j = 0; j < NT / 2; ++j) asm volatile("" : "+v"(csrc[j]));
@@ -424,11 +424,10 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
     // epilogue.  Sweep 1: the least upper bound U over the row's candidates so far.  Sweep 2: list
     // (ascending) the candidates whose lower bound is <= U, up to kListPerHalf per lane half; U only
     // shrinks over passes, so earlier listings are re-filtered at the end.
-    const float rho = __uint_as_float(lds_ratio[0]);
     const float hn = vn + en;       // >= |vh|
     const float vr = vn * inv_den;  // |r| of the row being assigned
-    const float K = 2.0f * inv_den * 1.000001f * (en + hn * rho + p.acc_rel * hn * (1.0f + rho)) + 2.0f * dr +
-                    4.8e-7f * vr;
+    const float A = 2.0f * inv_den * 1.000001f * (en + p.acc_rel * hn) + 2.0f * dr + 4.8e-7f * vr;
+    const float B = 2.0f * inv_den * 1.000001f * hn * (1.0f + p.acc_rel);
     const float m2 = -2.0f * inv_den;
     const float4* meta = lds_meta + 4 * h;
     const int kl_h = pbase + 4 * h;
@@ -440,9 +439,9 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int io = t * 32 + (v & 3) + 8 * (v >> 2);
-        const float4 m = meta[io];  // |c|^2 (inf for padding), |c|, e0
+        const float4 m = meta[io];  // |c|^2 (inf for padding), |c|, e0, |ec|
         const float sc = fmaf(m2, acc[t][v], m.x);
-        U = fminf(U, sc + fmaf(K, m.y, m.z));
+        U = fminf(U, sc + fmaf(A, m.y, fmaf(B, m.w, m.z)));
       }
     }
     U = fminf(U, __shfl_xor(U, 32));
@@ -454,7 +453,7 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
       for (int v = 0; v < 16; ++v) {
         const int kl = kl_h + t * 32 + (v & 3) + 8 * (v >> 2);
         const float4 m = meta[t * 32 + (v & 3) + 8 * (v >> 2)];
-        const float lb = fmaf(m2, acc[t][v], m.x) - fmaf(K, m.y, m.z);
+        const float lb = fmaf(m2, acc[t][v], m.x) - fmaf(A, m.y, fmaf(B, m.w, m.z));
         const bool q = lb <= U && kl < cnt;
         if (__builtin_amdgcn_ballot_w64(q)) {  // wave-uniform skip: most candidates qualify for no row
 #pragma unroll

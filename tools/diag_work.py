@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Diagnostics (GPU): histogram of rqsid_assign's re-score work items per encode level
 (n = listed candidates, -1 = every candidate, -2 = penalty) on the bench workload."""
+import os
 import sys
 from pathlib import Path
 
@@ -11,11 +12,12 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 from generative_ranking_recommender_amd import ops, synth  # noqa: E402
 import generative_ranking_recommender_amd.encode as encmod  # noqa: E402
 from generative_ranking_recommender_amd.encode import HIERARCHICAL_TRAIN, RQEncoder  # noqa: E402
+import bench  # noqa: E402
 
 
 def main(n=1_000_000, seed=99):
     dev = torch.device("cuda", 0)
-    cb = synth.encode_codebooks(seed=seed)
+    cb = bench.codebooks(os.environ.get("BENCH_CODEBOOKS", "fitted"), dev)
     enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], [128, 128, 256],
                     match=torch.from_numpy(cb["match"]), semantics=HIERARCHICAL_TRAIN, device=dev)
     x = torch.from_numpy(synth.mixture_rows(0, n)).to(dev)

@@ -16,7 +16,7 @@ from generative_ranking_recommender_amd.encode import HIERARCHICAL_TRAIN, RQEnco
 
 def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000)), reps=int(os.environ.get("SWEEP_REPS", 5))):
     dev = torch.device("cuda", 0)
-    cb = synth.encode_codebooks(seed=99)
+    cb = bench.codebooks(os.environ.get("BENCH_CODEBOOKS", "fitted"), dev)
     enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], [128, 128, 256],
                     match=torch.from_numpy(cb["match"]), semantics=HIERARCHICAL_TRAIN, device=dev)
     x = bench.make_rows(n, 0, dev)
