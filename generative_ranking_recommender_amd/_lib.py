@@ -74,11 +74,12 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not LIB_PATH.exists():
+    path = Path(os.environ.get("RQSID_LIB", LIB_PATH))  # A/B builds of the same ABI (tools/)
+    if not path.exists():
         raise RuntimeError(
-            f"HIP library {LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            f"HIP library {path} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
             "(there is no CPU fallback for the semantic-ID kernels)")
-    lib = ctypes.CDLL(str(LIB_PATH))
+    lib = ctypes.CDLL(str(path))
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

@@ -51,7 +51,7 @@ class PreparedCenters:
     """Centres + the derived data rqsid_assign reads (fp16 copy and screening-bound norms)."""
     centers: torch.Tensor      # f32 [K, D]
     c16: torch.Tensor          # int16 [K, D] (IEEE half bits; out-of-normal-range values stored as 0)
-    meta: torch.Tensor         # f32 [K, 4]: |c|^2, |c|, |c - c16|, |c16|
+    meta: torch.Tensor         # f32 [K, 4]: |c|^2, |c|, |c - c16 2^-s|, 2^-s (table scale)
 
     @property
     def k(self) -> int:

@@ -38,10 +38,10 @@ extern "C" {
 int rqsid_version(void);
 const char* rqsid_last_error(void);
 
-/* Centre preparation for rqsid_assign: every centre rounded to fp16 (values outside the fp16
- * normal range stored as 0) in c16 [k][dim] (IEEE half bits), and c_meta[k][4] =
- * {|c|^2, |c|, |c - c16|, |c16|} (fp64-accumulated; the last three feed the screening error
- * bound).  Replaces the per-call centre side of torch.cdist's mm-expansion (ATen
+/* Centre preparation for rqsid_assign: the table scaled by a power of two 2^s (largest element just
+ * below 2^14) and rounded to fp16, scaled values outside the fp16 normal range stored as 0, in
+ * c16 [k][dim] (IEEE half bits), and c_meta[k][4] = {|c|^2, |c|, |c - c16 2^-s|, 2^-s}
+ * (fp64-accumulated; |c| and the residual feed the screening error bound).  Replaces the per-call centre side of torch.cdist's mm-expansion (ATen
  * _euclidean_dist) used by pairwise_distance_full, balancekmeans/__init__.py:576-603. */
 int rqsid_prepare_centers(const float* centers, int64_t k, int32_t dim,
                           uint16_t* c16, float* c_meta, void* stream);

@@ -81,6 +81,37 @@ def test_nearest_forced_near_ties():
     assert got[2] == 3 and got[3] == 4 and got[4] == 11
 
 
+@pytest.mark.parametrize("xs,cs", [(1e-6, 1.0), (1.0, 1e-6), (1e-7, 1e-7), (3e3, 1.0), (1.0, 2e3)])
+def test_nearest_extreme_scales(xs, cs):
+    """Rows / centres far from unit scale: their fp16 images are mostly subnormal (flushed: the
+    MFMA would otherwise align products to the subnormal's nominal exponent) or near the fp16
+    range; the table scale and the measured residuals keep the screen's bound rigorous."""
+    rng = np.random.default_rng(int(xs * 1e3 + cs))
+    c = (rng.standard_normal((200, 512)) * cs).astype(np.float32)
+    c[100:] *= np.float32(1e-3)                  # mixed centre norms in one table
+    x = (rng.standard_normal((3000, 512)) * xs).astype(np.float32)
+    x[:1000] = c[rng.integers(0, 200, 1000)] + (0.05 * cs * rng.standard_normal((1000, 512))).astype(np.float32)
+    got = ops.nearest(gpu(x), ops.prepare_centers(gpu(c))).cpu().numpy()
+    assert (got == exact_ids(x, c)).all()
+
+
+def test_prepare_centers_table_scale():
+    """c16 holds c 2^s with the largest |c 2^s| in [2^13, 2^14), no subnormals; meta = {|c|^2, |c|,
+    |c - c16 2^-s|, 2^-s}."""
+    rng = np.random.default_rng(5)
+    c = (rng.standard_normal((300, 256)) * 3e-3).astype(np.float32)
+    pc = ops.prepare_centers(gpu(c))
+    meta = pc.meta.cpu().numpy()
+    h = pc.c16.cpu().numpy().view(np.float16).astype(np.float64).reshape(300, 256)
+    scale = meta[0, 3]
+    assert (meta[:, 3] == scale).all() and np.log2(scale) == np.round(np.log2(scale))
+    assert 2.0 ** 13 <= np.abs(h).max() < 2.0 ** 14
+    assert ((np.abs(h) >= 2.0 ** -14) | (h == 0)).all()
+    res = np.sqrt(((c.astype(np.float64) - h * scale) ** 2).sum(1))
+    assert np.all(meta[:, 2] >= res) and np.allclose(meta[:, 2], res, rtol=1e-6)
+    assert np.allclose(meta[:, 0], (c.astype(np.float64) ** 2).sum(1), rtol=1e-6)
+
+
 @pytest.mark.parametrize("gd,norm", [([512], True), ([128, 384], True), ([512], False), ([100, 12, 400], True)])
 def test_residual(gd, norm):
     x = synth.small_mixture(3000, m=30, seed=4)
