@@ -36,7 +36,7 @@ SIGNATURES = {
                              c_vp, c_vp, c_vp, c_i32,
                              c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
                              c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                             c_vp, c_vp, c_vp, c_i64, c_vp]),
+                             c_vp, c_vp, c_i32, c_vp, c_i64, c_vp]),
     "rqsid_residual": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "rqsid_scale_groups": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp]),
     "rqsid_centroid_tile_rows": (c_i32, []),

@@ -67,8 +67,8 @@ struct AssignParams {
   const int32_t* seg_row_off;
   const int32_t* seg_tile_off;
   const float* centers;
-  const uint16_t* c16;   // fp16 bits [k][dim] (rqsid_prepare_centers)
-  const float* c_meta;   // float4 per centre: |c|^2, |c|, |c - c16 2^-s|, 2^-s (the table scale)
+  const uint16_t* c16;   // fp16 bits [2][k][dim]: hi, lo tables (rqsid_prepare_centers)
+  const float* c_meta;   // [k+1] float4: per centre |c|^2, |c|, |c - (hi + lo 2^-12) 2^-s|, |c - hi 2^-s|; row k: 2^-s
   int32_t n_centers;
   const int32_t* cand_base;
   const int32_t* cand_count;
@@ -81,6 +81,7 @@ struct AssignParams {
   int32_t* work_count;
   int64_t work_cap;
   float acc_rel;
+  int32_t terms;          // 1 or 3 (screen product terms; host-side dispatch only)
   const float* ca;
   const int32_t* seg_ca;
   const float* cb;
@@ -132,42 +133,42 @@ __device__ __forceinline__ int table_scale_exp(unsigned maxbits) {
 // ---------------------------------------------------------------------------
 // centre preparation
 // ---------------------------------------------------------------------------
-// meta[0].w holds the absmax bits while this runs (centers_absmax_kernel) and is rewritten to 2^-s
-// by centers_scale_kernel afterwards; every other row's .w gets 2^-s here.
+// c16 = [hi | lo] tables: hi = fp16(c 2^s), lo = fp16((c 2^s - hi) 2^12) (the 3-term screen's second
+// term; scaled by 2^12 so it stays in the fp16 normal range).  meta[k] = {|c|^2, |c|,
+// |c - (hi + lo 2^-12) 2^-s|, |c - hi 2^-s|}; meta[k_total].x holds the absmax bits while this runs
+// (centers_absmax_kernel) and 2^-s afterwards (centers_scale_kernel).
 __global__ __launch_bounds__(256) void prepare_centers_kernel(const float* __restrict__ c, int64_t k, int dim,
                                                               _Float16* __restrict__ c16, float4* __restrict__ meta) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= k) return;
-  const int sx = table_scale_exp(reinterpret_cast<const unsigned*>(meta)[3]);
+  const int sx = table_scale_exp(reinterpret_cast<const unsigned*>(meta + k)[0]);
   const float* cr = c + row * dim;
-  double s = 0.0, se = 0.0;
+  double s = 0.0, s1 = 0.0, s2 = 0.0;
   for (int i = lane; i < dim; i += 64) {
     const float v = cr[i];
-    const _Float16 hv = to_f16(ldexpf(v, sx));
-    const double ed = (double)v - ldexp((double)(float)hv, -sx);  // exact: the residual of what the MFMA sees
+    const float vs = ldexpf(v, sx);
+    const _Float16 hv = to_f16(vs);
+    const float r1 = vs - (float)hv;  // exact (or vs itself when hv was flushed)
+    const _Float16 lv = to_f16(r1 * 4096.0f);
     c16[row * dim + i] = hv;
+    c16[(k + row) * dim + i] = lv;
+    const double e1 = (double)v - ldexp((double)(float)hv, -sx);  // exact residuals of what the MFMA sees
+    const double e2 = e1 - ldexp((double)(float)lv, -sx - 12);
     s += (double)v * (double)v;
-    se += ed * ed;
+    s1 += e1 * e1;
+    s2 += e2 * e2;
   }
   s = wave_sum(s);
-  se = wave_sum(se);
-  if (lane == 0) {  // norms rounded up slightly: they only feed the screening bound
-    const float4 m = make_float4((float)s, (float)sqrt(s) * 1.0000002f, (float)sqrt(se) * 1.0000002f,
-                                 ldexpf(1.0f, -sx));
-    if (row == 0) {
-      float* m0 = reinterpret_cast<float*>(meta);
-      m0[0] = m.x;
-      m0[1] = m.y;
-      m0[2] = m.z;
-    } else {
-      meta[row] = m;
-    }
-  }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane == 0)  // norms rounded up slightly: they only feed the screening bound
+    meta[row] = make_float4((float)s, (float)sqrt(s) * 1.0000002f, (float)sqrt(s2) * 1.0000002f,
+                            (float)sqrt(s1) * 1.0000002f);
 }
 
-__global__ void centers_scale_kernel(float* __restrict__ meta0w) {
-  *meta0w = ldexpf(1.0f, -table_scale_exp(__float_as_uint(*meta0w)));
+__global__ void centers_scale_kernel(float* __restrict__ scale) {
+  *scale = ldexpf(1.0f, -table_scale_exp(__float_as_uint(*scale)));
 }
 
 // ---------------------------------------------------------------------------
@@ -213,9 +214,10 @@ __device__ __forceinline__ void wait_chunks(int younger) {
 // ---------------------------------------------------------------------------
 // screening kernel
 // ---------------------------------------------------------------------------
-template <int NT, int S>
+template <int NT, int S, bool T3>
 struct ScreenLayout {
-  static constexpr int kCStage = NT * 32 * 64;  // NT*32 candidates x 32 fp16 dims
+  static constexpr int kCHalf = NT * 32 * 64;              // NT*32 candidates x 32 fp16 dims
+  static constexpr int kCStage = kCHalf * (T3 ? 2 : 1);     // hi (+ lo) centre images
   static constexpr int kStage = kXStage + kCStage;
   static constexpr int kMeta = S * kStage;       // float4 {|c|^2, |c|, e0, 0} per candidate of the pass
   static constexpr int kRes = kMeta + NT * 32 * 16;        // residual rows ca, cb (fp32, dim each)
@@ -246,12 +248,16 @@ __device__ __forceinline__ void push_work(const AssignParams& p, bool need, int 
 // (|ch_k| <= |c_k| + |ec_k|; dr = the rounding of the reference's r = v/den).  The centre term is per
 // candidate: a near-zero centroid (large RELATIVE fp16 error, tiny absolute error) loosens only its own
 // bound.
+// Three-term screen (T3): v = vh + vl 2^-12 + ev and c 2^s = ch + cl 2^-12 + ec; the MFMAs sum
+// vh.ch (acc) and vl.ch + vh.cl (accl, its own accumulator) and the omitted vl.cl, (vh + vl).ec and
+// ev.c terms plus both accumulations are charged per candidate against |c|, |ec2| = |c - (ch + cl
+// 2^-12) 2^-s| and |ec1| = |c - ch 2^-s| (see the epilogue's A, B, C).
 inline float accumulation_rel(int dim) { return (float)(((dim / 16) * 17.0 + 8.0) * std::ldexp(1.0, -23) * 1.02); }
 
-template <int NT, int S, int RL, bool NORM>
-__global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <= 3) ? 2 : 1)) void assign_screen_kernel(AssignParams p) {
-  using L = ScreenLayout<NT, S>;
-  constexpr int P = 4 + NT / 2;  // DMA ops per wave per chunk (x: 4, centres: NT/2)
+template <int NT, int S, int RL, bool NORM, bool T3>
+__global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <= 3) ? 2 : 1))) void assign_screen_kernel(AssignParams p) {
+  using L = ScreenLayout<NT, S, T3>;
+  constexpr int P = 4 + (NT / 2) * (T3 ? 2 : 1);  // DMA ops per wave per chunk (x: 4, centres: NT/2 per table)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // FP16 (and FP64) denormals flushed: a row value below the fp16 normal range converts to 0 (its
   // value lands in the measured |v - vh|), so no subnormal operand reaches the MFMA (to_f16)
@@ -332,7 +338,8 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
   }
   double sv2 = 0.0;            // sum v^2 in fp64 (NORM: the normalising denominator is exact)
   f2 sf2v = {0.f, 0.f}, se2v = {0.f, 0.f};  // sum v^2 (fp32, bound only), sum (v - fp16(v))^2
-  float vn = 0.f, en = 0.f, inv_den = 1.f, dr = 0.f;
+  f2 se2l = {0.f, 0.f};                      // T3: sum of the second term's residual^2 (units 2^-12)
+  float vn = 0.f, en = 0.f, en2 = 0.f, inv_den = 1.f, dr = 0.f;
   float4* lds_meta = reinterpret_cast<float4*>(smem + L::kMeta);
   const f32x16 zero16 = {};
   const int xsw = (r >> 1) & 7;  // swizzle of this lane's row in the x image
@@ -343,6 +350,7 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
     const int pbase = pass * NT * 32;
     // centre DMA sources: instruction j covers candidates (wave*NT/2 + j)*16 + lane/4, slot lane%4
     const _Float16* csrc[NT / 2];
+    const _Float16* clo[T3 ? NT / 2 : 1];
 #pragma unroll
     for (int j = 0; j < NT / 2; ++j) {
       const int il = (wave * (NT / 2) + j) * 16 + (lane >> 2);
@@ -350,23 +358,29 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
       const int cg = cand_global(p, cbase, kl);
       const int slot = (lane & 3) ^ ((il >> 2) & 3);
       csrc[j] = reinterpret_cast<const _Float16*>(p.c16) + (int64_t)cg * dim + slot * 8;
+      if (T3) clo[j] = csrc[j] + (int64_t)p.n_centers * dim;
     }
     __syncthreads();
     if (tid < NT * 32) {
       const bool live = pbase + tid < cnt;
       const int kl = live ? pbase + tid : cnt - 1;
       const float4 m = reinterpret_cast<const float4*>(p.c_meta)[cand_global(p, cbase, kl)];
-      // {|c|^2, |c|, e0 = the fp32 epilogue's own rounding allowance, |c - c16|}; padding candidates
-      // get |c|^2 = inf
-      lds_meta[tid] = make_float4(live ? m.x : INFINITY, m.y, fmaf(2.39e-7f, m.x, 1e-30f), m.z);
+      // {|c|^2 (inf for padding candidates), |c|, |ec2| (T3) or |ec1|, |ec1|}
+      lds_meta[tid] = make_float4(live ? m.x : INFINITY, m.y, T3 ? m.z : m.w, m.w);
     }
 #pragma unroll
-    for (int j = 0; j < NT / 2; ++j) asm volatile("" : "+v"(csrc[j]));
+    for (int j = 0; j < NT / 2; ++j) {
+      asm volatile("" : "+v"(csrc[j]));
+      if (T3) asm volatile("" : "+v"(clo[j]));
+    }
     __syncthreads();
 
     f32x16 acc[NT];
+    f32x16 accl[T3 ? NT : 1];  // T3: vl.ch + vh.cl in units of 2^-12
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = zero16;
+#pragma unroll
+    for (int t = 0; t < (T3 ? NT : 1); ++t) accl[t] = zero16;
 
     auto issue = [&](int c) {
       const uint32_t sb = lds0 + (uint32_t)((c % S) * L::kStage);
@@ -376,6 +390,12 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
 #pragma unroll
       for (int j = 0; j < NT / 2; ++j)
         dma16(csrc[j] + c * kChunk, __builtin_amdgcn_readfirstlane(sb + kXStage + (wave * (NT / 2) + j) * 1024));
+      if (T3) {
+#pragma unroll
+        for (int j = 0; j < NT / 2; ++j)
+          dma16(clo[j] + c * kChunk,
+                __builtin_amdgcn_readfirstlane(sb + kXStage + L::kCHalf + (wave * (NT / 2) + j) * 1024));
+      }
     };
     auto compute = [&](int c) {
       const unsigned char* xb = smem + (c % S) * L::kStage + wave * kXWaveBytes + r * 128;
@@ -405,12 +425,27 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = (NORM ? v[e] * inv1 : v[e]) - bv[e];
         }
-        h2 hh[4];
+        h2 hh[4], lh[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) hh[e] = __builtin_convertvector(v[e], h2);
         const f16x8 bf = __builtin_shufflevector(__builtin_shufflevector(hh[0], hh[1], 0, 1, 2, 3),
                                                  __builtin_shufflevector(hh[2], hh[3], 0, 1, 2, 3),
                                                  0, 1, 2, 3, 4, 5, 6, 7);
+        if (T3) {  // second term: the fp16 rounding residual scaled by 2^12 (fp16 normal range)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const f2 xs = (v[e] - __builtin_convertvector(hh[e], f2)) * 4096.0f;  // exact
+            lh[e] = __builtin_convertvector(xs, h2);
+            if (pass == 0) {
+              const f2 ev = xs - __builtin_convertvector(lh[e], f2);  // exact
+              se2l = ev * ev + se2l;
+            }
+          }
+        }
+        f16x8 bl = {};
+        if (T3)
+          bl = __builtin_shufflevector(__builtin_shufflevector(lh[0], lh[1], 0, 1, 2, 3),
+                                       __builtin_shufflevector(lh[2], lh[3], 0, 1, 2, 3), 0, 1, 2, 3, 4, 5, 6, 7);
         if (pass == 0) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -429,6 +464,11 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
         for (int t = 0; t < NT; ++t) {
           const f16x8 af = *reinterpret_cast<const f16x8*>(cbp + t * 32 * 64 + (qa << 4));
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[t], 0, 0, 0);
+          if (T3) {
+            const f16x8 al = *reinterpret_cast<const f16x8*>(cbp + L::kCHalf + t * 32 * 64 + (qa << 4));
+            accl[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bl, accl[t], 0, 0, 0);
+            accl[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bf, accl[t], 0, 0, 0);
+          }
         }
       }
     };
@@ -447,6 +487,10 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
       const float se2 = se2v.x + se2v.y, sf2 = sf2v.x + sf2v.y;
       const float e2 = se2 + __shfl_xor(se2, 32);
       en = sqrtf(e2) * 1.001f + 1e-30f;
+      if (T3) {
+        const float l2 = se2l.x + se2l.y;
+        en2 = sqrtf(l2 + __shfl_xor(l2, 32)) * (1.001f / 4096.0f) + 1e-30f;
+      }
       float nrm;
       if (NORM && RL >= 1) {
         const double tot = sv2 + __shfl_xor(sv2, 32);
@@ -467,10 +511,15 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
     // shrinks over passes, so earlier listings are re-filtered at the end.
     const float hn = vn + en;       // >= |vh|
     const float vr = vn * inv_den;  // |r| of the row being assigned
-    const float A = 2.0f * inv_den * 1.000001f * (en + p.acc_rel * hn) + 2.0f * dr + 4.8e-7f * vr;
-    const float B = 2.0f * inv_den * 1.000001f * hn * (1.0f + p.acc_rel);
+    const float ar = p.acc_rel, k2 = 2.0f * inv_den * 1.000001f;
+    // e_k = A |c_k| + B m.z + C |ec1_k| + e0(|c_k|^2): 1-term m.z = |ec1| and C = 0; T3 m.z = |ec2|
+    const float A = T3 ? k2 * (en2 + ar * (hn + en + en2)) + 2.0f * dr + 7.2e-7f * vr
+                       : k2 * (en + ar * hn) + 2.0f * dr + 4.8e-7f * vr;
+    const float B = T3 ? k2 * (hn * (1.0f + ar) + 2.0f * (en + en2)) : k2 * hn * (1.0f + ar);
+    const float C = T3 ? k2 * ((en + en2) + ar * (2.0f * hn + en + en2)) : 0.0f;
     // the MFMA sums are in units of 2^s of the centre table (rqsid_prepare_centers; exact power of two)
-    const float m2 = -2.0f * inv_den * __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(p.c_meta[3])));
+    const float m2 = -2.0f * inv_den *
+                     __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(p.c_meta[4 * p.n_centers])));
     const float4* meta = lds_meta + 4 * h;
     const int kl_h = pbase + 4 * h;
     // sweep 1: U = least upper bound.  The scheduling barriers stop hipcc from hoisting every
@@ -481,9 +530,11 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int io = t * 32 + (v & 3) + 8 * (v >> 2);
-        const float4 m = meta[io];  // |c|^2 (inf for padding), |c|, e0, |ec|
-        const float sc = fmaf(m2, acc[t][v], m.x);
-        U = fminf(U, sc + fmaf(A, m.y, fmaf(B, m.w, m.z)));
+        const float4 m = meta[io];
+        const float dot = T3 ? fmaf(0x1p-12f, accl[t][v], acc[t][v]) : acc[t][v];
+        const float sc = fmaf(m2, dot, m.x);
+        const float e0 = fmaf(2.39e-7f, m.x, 1e-30f);  // the fp32 epilogue's own rounding
+        U = fminf(U, sc + fmaf(A, m.y, fmaf(B, m.z, T3 ? fmaf(C, m.w, e0) : e0)));
       }
     }
     U = fminf(U, __shfl_xor(U, 32));
@@ -495,7 +546,9 @@ __global__ __launch_bounds__(256, S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <=
       for (int v = 0; v < 16; ++v) {
         const int kl = kl_h + t * 32 + (v & 3) + 8 * (v >> 2);
         const float4 m = meta[t * 32 + (v & 3) + 8 * (v >> 2)];
-        const float lb = fmaf(m2, acc[t][v], m.x) - fmaf(A, m.y, fmaf(B, m.w, m.z));
+        const float dot = T3 ? fmaf(0x1p-12f, accl[t][v], acc[t][v]) : acc[t][v];
+        const float e0 = fmaf(2.39e-7f, m.x, 1e-30f);
+        const float lb = fmaf(m2, dot, m.x) - fmaf(A, m.y, fmaf(B, m.z, T3 ? fmaf(C, m.w, e0) : e0));
         const bool q = lb <= U && kl < cnt;
         if (__builtin_amdgcn_ballot_w64(q)) {  // wave-uniform skip: most candidates qualify for no row
 #pragma unroll
@@ -753,14 +806,14 @@ __global__ __launch_bounds__(64) void mfma_probe_kernel(const uint16_t* __restri
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-template <int NT, int S>
+template <int NT, int S, bool T3>
 void set_attrs(bool* ok) {
-  const int bytes = ScreenLayout<NT, S>::kMaxBytes;
-  const void* ks[] = {(const void*)assign_screen_kernel<NT, S, 0, false>,
-                      (const void*)assign_screen_kernel<NT, S, 1, false>,
-                      (const void*)assign_screen_kernel<NT, S, 1, true>,
-                      (const void*)assign_screen_kernel<NT, S, 2, false>,
-                      (const void*)assign_screen_kernel<NT, S, 2, true>};
+  const int bytes = ScreenLayout<NT, S, T3>::kMaxBytes;
+  const void* ks[] = {(const void*)assign_screen_kernel<NT, S, 0, false, T3>,
+                      (const void*)assign_screen_kernel<NT, S, 1, false, T3>,
+                      (const void*)assign_screen_kernel<NT, S, 1, true, T3>,
+                      (const void*)assign_screen_kernel<NT, S, 2, false, T3>,
+                      (const void*)assign_screen_kernel<NT, S, 2, true, T3>};
   for (const void* k : ks)
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) *ok = false;
 }
@@ -778,25 +831,27 @@ bool g_attr_done = false;
 int ensure_attrs() {
   if (g_attr_done) return RQSID_OK;
   bool ok = true;
-  set_attrs<4, 3>(&ok);
-  set_attrs<4, 6>(&ok);
-  set_attrs<8, 4>(&ok);
-  set_attrs<8, 3>(&ok);
-  set_attrs<4, 2>(&ok);
-  set_attrs<8, 2>(&ok);
+  set_attrs<4, 3, false>(&ok);
+  set_attrs<4, 6, false>(&ok);
+  set_attrs<8, 4, false>(&ok);
+  set_attrs<8, 3, false>(&ok);
+  set_attrs<4, 2, false>(&ok);
+  set_attrs<8, 2, false>(&ok);
+  set_attrs<4, 2, true>(&ok);
+  set_attrs<4, 3, true>(&ok);
   if (!ok) return fail(RQSID_E_LAUNCH, "assign: cannot raise the dynamic LDS limit");
   g_attr_done = true;
   return RQSID_OK;
 }
 
-template <int NT, int S>
+template <int NT, int S, bool T3>
 void launch_screen(const AssignParams& p, int rl, bool norm, unsigned grid, hipStream_t st) {
-  const size_t lds = ScreenLayout<NT, S>::bytes(rl, p.dim);
-  if (rl == 0) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 0, false>), dim3(grid), dim3(256), lds, st, p);
-  else if (rl == 1 && norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, true>), dim3(grid), dim3(256), lds, st, p);
-  else if (rl == 1) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, false>), dim3(grid), dim3(256), lds, st, p);
-  else if (norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, true>), dim3(grid), dim3(256), lds, st, p);
-  else hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, false>), dim3(grid), dim3(256), lds, st, p);
+  const size_t lds = ScreenLayout<NT, S, T3>::bytes(rl, p.dim);
+  if (rl == 0) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 0, false, T3>), dim3(grid), dim3(256), lds, st, p);
+  else if (rl == 1 && norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, true, T3>), dim3(grid), dim3(256), lds, st, p);
+  else if (rl == 1) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, false, T3>), dim3(grid), dim3(256), lds, st, p);
+  else if (norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, true, T3>), dim3(grid), dim3(256), lds, st, p);
+  else hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, false, T3>), dim3(grid), dim3(256), lds, st, p);
 }
 
 }  // namespace
@@ -812,15 +867,15 @@ int rqsid_prepare_centers(const float* centers, int64_t k, int32_t dim, uint16_t
     return fail(RQSID_E_ARG, "prepare_centers: bad arguments (k=%lld dim=%d)", (long long)k, dim);
   if (k == 0) return RQSID_OK;
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(c_meta + 3, 0, sizeof(float), st) != hipSuccess)
+  float* scale = c_meta + 4 * k;  // row k of meta
+  if (hipMemsetAsync(scale, 0, 4 * sizeof(float), st) != hipSuccess)
     return fail(RQSID_E_LAUNCH, "prepare_centers: hipMemsetAsync failed");
   const int64_t n = k * dim;
   const unsigned g = (unsigned)(cdiv(n, 256 * 16) < 2048 ? cdiv(n, 256 * 16) : 2048);
-  hipLaunchKernelGGL(centers_absmax_kernel, dim3(g), dim3(256), 0, st, centers, n,
-                     reinterpret_cast<unsigned*>(c_meta + 3));
+  hipLaunchKernelGGL(centers_absmax_kernel, dim3(g), dim3(256), 0, st, centers, n, reinterpret_cast<unsigned*>(scale));
   hipLaunchKernelGGL(prepare_centers_kernel, dim3((unsigned)cdiv(k, 4)), dim3(256), 0, st,
                      centers, k, dim, reinterpret_cast<_Float16*>(c16), reinterpret_cast<float4*>(c_meta));
-  hipLaunchKernelGGL(centers_scale_kernel, dim3(1), dim3(1), 0, st, c_meta + 3);
+  hipLaunchKernelGGL(centers_scale_kernel, dim3(1), dim3(1), 0, st, scale);
   return check_launch("prepare_centers");
 }
 
@@ -836,12 +891,12 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
                  const int32_t* cand_count, int32_t cand_count_max, const int32_t* cand_idx,
                  const int32_t* cand_lid, const uint8_t* seg_flags, int32_t res_levels, int32_t res_normalize, const float* ca,
                  const int32_t* seg_ca, const float* cb, const int32_t* seg_cb, const float* den_in,
-                 float* den_out, int32_t* out_local, int32_t* out_global, void* workspace,
+                 float* den_out, int32_t* out_local, int32_t* out_global, int32_t screen_terms, void* workspace,
                  int64_t workspace_bytes, void* stream) {
   if (dim <= 0 || dim % kChunk || dim > kMaxDim || n_rows < 0 || n_segments <= 0 || !seg_row_off ||
       !seg_tile_off || !centers || !c16 || !c_meta || !cand_base || !cand_count || !out_local || !out_global ||
       n_centers <= 0 || cand_count_max < 0 || max_tiles < 0 || n_rows > INT32_MAX || res_levels < 0 ||
-      res_levels > 2)
+      res_levels > 2 || (screen_terms != 0 && screen_terms != 1 && screen_terms != 3))
     return fail(RQSID_E_ARG, "assign: bad arguments (n=%lld dim=%d S=%d K=%d levels=%d)", (long long)n_rows, dim,
                 n_segments, n_centers, res_levels);
   if ((res_levels >= 1 && !ca) || (res_levels == 2 && (!cb || !seg_cb || (res_normalize && !den_in))))
@@ -887,15 +942,24 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   // Measured on MI355X (tools/screen_sweep.py): independent blocks per CU beat ring depth: NT4 with
   // S=2 runs 3 blocks/CU, NT8 with S=2 runs 2 blocks/CU (RQSID_SCREEN_VARIANT=1/3 select the older
   // deeper-ring single-block configurations for comparison).
+  // Terms: the 3-term screen (rounding residuals of both operands summed by two more MFMAs) shrinks
+  // the bound ~5x at 2 blocks/CU; auto picks it for residual levels with <= 128 candidates, where
+  // trained codebooks leave the most rows inside the 1-term bound ("Screen terms").
   const int v = screen_variant();
-  if (cand_count_max <= 128) {
-    if (v == 1) launch_screen<4, 6>(p, res_levels, norm, grid, st);
-    else if (v == 3) launch_screen<4, 3>(p, res_levels, norm, grid, st);
-    else launch_screen<4, 2>(p, res_levels, norm, grid, st);
+  // (The 8-tile form has no 3-term build: its second accumulator set does not fit 256 VGPRs.)
+  const bool t3 = cand_count_max <= 128 && (screen_terms == 3 || (screen_terms == 0 && res_levels >= 1));
+  p.terms = t3 ? 3 : 1;
+  if (t3) {
+    if (v == 3) launch_screen<4, 3, true>(p, res_levels, norm, grid, st);
+    else launch_screen<4, 2, true>(p, res_levels, norm, grid, st);
+  } else if (cand_count_max <= 128) {
+    if (v == 1) launch_screen<4, 6, false>(p, res_levels, norm, grid, st);
+    else if (v == 3) launch_screen<4, 3, false>(p, res_levels, norm, grid, st);
+    else launch_screen<4, 2, false>(p, res_levels, norm, grid, st);
   } else {
-    if (v == 1) launch_screen<8, 3>(p, res_levels, norm, grid, st);
-    else if (v == 3) launch_screen<8, 4>(p, res_levels, norm, grid, st);
-    else launch_screen<8, 2>(p, res_levels, norm, grid, st);
+    if (v == 1) launch_screen<8, 3, false>(p, res_levels, norm, grid, st);
+    else if (v == 3) launch_screen<8, 4, false>(p, res_levels, norm, grid, st);
+    else launch_screen<8, 2, false>(p, res_levels, norm, grid, st);
   }
   if ((rc = check_launch("assign_screen"))) return rc;
   const dim3 g(4096);  // multiple of 8 (XCD-grouped work runs)

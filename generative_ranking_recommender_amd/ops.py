@@ -50,8 +50,8 @@ def centroid_tile_rows() -> int:
 class PreparedCenters:
     """Centres + the derived data rqsid_assign reads (fp16 copy and screening-bound norms)."""
     centers: torch.Tensor      # f32 [K, D]
-    c16: torch.Tensor          # int16 [K, D] (IEEE half bits; out-of-normal-range values stored as 0)
-    meta: torch.Tensor         # f32 [K, 4]: |c|^2, |c|, |c - c16 2^-s|, 2^-s (table scale)
+    c16: torch.Tensor          # int16 [2, K, D]: hi, lo fp16 terms of c 2^s (IEEE half bits)
+    meta: torch.Tensor         # f32 [K+1, 4]: |c|^2, |c|, |2-term residual|, |1-term residual|; row K: 2^-s
 
     @property
     def k(self) -> int:
@@ -59,15 +59,15 @@ class PreparedCenters:
 
     @property
     def sqnorm(self) -> torch.Tensor:
-        return self.meta[:, 0]
+        return self.meta[:-1, 0]
 
 
 def prepare_centers(c: torch.Tensor) -> PreparedCenters:
     c = c.float().contiguous()
     _require_device(c)
     k, d = c.shape
-    c16 = torch.empty((k, d), dtype=torch.int16, device=c.device)
-    meta = torch.empty((k, 4), dtype=torch.float32, device=c.device)
+    c16 = torch.empty((2, k, d), dtype=torch.int16, device=c.device)
+    meta = torch.empty((k + 1, 4), dtype=torch.float32, device=c.device)
     _lib.check(lib().rqsid_prepare_centers(_ptr(c), k, d, _ptr(c16), _ptr(meta), _stream()),
                "rqsid_prepare_centers")
     return PreparedCenters(c, c16, meta)
@@ -208,8 +208,10 @@ class FusedResidual:
 
 def assign(x: torch.Tensor, pc: PreparedCenters, buckets: Buckets, cand: Candidates,
            out_local: Optional[torch.Tensor] = None, out_global: Optional[torch.Tensor] = None,
-           workspace: Optional[AssignWorkspace] = None, fused: Optional[FusedResidual] = None):
-    """Exact segmented argmin. Returns (local i32[N], global i32[N])."""
+           workspace: Optional[AssignWorkspace] = None, fused: Optional[FusedResidual] = None,
+           screen_terms: int = 0):
+    """Exact segmented argmin. Returns (local i32[N], global i32[N]).  ``screen_terms`` (0 auto, 1, 3)
+    only changes how much work the exact answer takes."""
     _require_device(x, pc.centers, cand.base, cand.count, cand.idx, cand.flags)
     n, d = x.shape
     if d != pc.centers.shape[1]:
@@ -233,17 +235,19 @@ def assign(x: torch.Tensor, pc: PreparedCenters, buckets: Buckets, cand: Candida
         None if f is None else _ptr(f.ca), None if f is None else _ptr(f.seg_ca),
         None if f is None else _ptr(f.cb), None if f is None else _ptr(f.seg_cb),
         None if f is None else _ptr(f.den_in), None if f is None else _ptr(f.den_out),
-        _ptr(out_local), _ptr(out_global), _ptr(workspace.buf), workspace.bytes, _stream()), "rqsid_assign")
+        _ptr(out_local), _ptr(out_global), int(screen_terms), _ptr(workspace.buf), workspace.bytes, _stream()),
+        "rqsid_assign")
     return out_local, out_global
 
 
-def nearest(x: torch.Tensor, pc: PreparedCenters, workspace: Optional[AssignWorkspace] = None) -> torch.Tensor:
+def nearest(x: torch.Tensor, pc: PreparedCenters, workspace: Optional[AssignWorkspace] = None,
+            screen_terms: int = 0) -> torch.Tensor:
     """Unconstrained nearest centre (KMeans.predict / pairwise_distance_full + argmin)."""
     n = x.shape[0]
     b = single_segment(n, x.device)
     cand = Candidates(torch.zeros(1, dtype=torch.int32, device=x.device),
                       torch.full((1,), pc.k, dtype=torch.int32, device=x.device), pc.k)
-    return assign(x, pc, b, cand, workspace=workspace)[1]
+    return assign(x, pc, b, cand, workspace=workspace, screen_terms=screen_terms)[1]
 
 
 def _groups_tensor(group_dims: Sequence[int], device) -> torch.Tensor:

@@ -38,11 +38,14 @@ extern "C" {
 int rqsid_version(void);
 const char* rqsid_last_error(void);
 
-/* Centre preparation for rqsid_assign: the table scaled by a power of two 2^s (largest element just
- * below 2^14) and rounded to fp16, scaled values outside the fp16 normal range stored as 0, in
- * c16 [k][dim] (IEEE half bits), and c_meta[k][4] = {|c|^2, |c|, |c - c16 2^-s|, 2^-s}
- * (fp64-accumulated; |c| and the residual feed the screening error bound).  Replaces the per-call centre side of torch.cdist's mm-expansion (ATen
- * _euclidean_dist) used by pairwise_distance_full, balancekmeans/__init__.py:576-603. */
+/* Centre preparation for rqsid_assign.  The table is scaled by a power of two 2^s (largest element
+ * just below 2^14) and split into two fp16 terms: hi = fp16(c 2^s) and lo = fp16((c 2^s - hi) 2^12),
+ * scaled values outside the fp16 normal range stored as 0 (the MFMA must never see a subnormal).
+ * c16 [2][k][dim] (IEEE half bits: the hi table, then the lo table); c_meta [k+1][4]: row j <  k =
+ * {|c|^2, |c|, |c - (hi + lo 2^-12) 2^-s|, |c - hi 2^-s|} (fp64-accumulated, feeding the screening
+ * error bound), row k = {2^-s, 0, 0, 0}.  Replaces the per-call centre side of torch.cdist's
+ * mm-expansion (ATen _euclidean_dist) used by pairwise_distance_full,
+ * balancekmeans/__init__.py:576-603. */
 int rqsid_prepare_centers(const float* centers, int64_t k, int32_t dim,
                           uint16_t* c16, float* c_meta, void* stream);
 
@@ -89,7 +92,11 @@ int32_t rqsid_assign_tile_rows(void);
  * (l1,l2) group) determines the parent IDs whose centres are subtracted.
  *
  * Method: fp16 MFMA screening (v_mfma_f32_32x32x16_f16) with a rigorous per-candidate error
- * bound, then an fp64 re-score of every row whose bound admits more than one candidate. */
+ * bound, then an fp64 re-score of every row whose bound admits more than one candidate.
+ * screen_terms: 1 = vh.ch only; 3 = vh.ch + vl.ch + vh.cl (both operands' fp16 rounding
+ * residuals, a ~5x tighter bound for 3x the MFMA work; segments of <= 128 candidates only, wider
+ * ones use 1); 0 = automatic (3 for residual levels with <= 128 candidates per segment).  The result
+ * never depends on it, only the speed. */
 int64_t rqsid_assign_workspace_bytes(int64_t n_rows);
 int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row_index,
                  int32_t n_segments, const int32_t* seg_row_off, const int32_t* seg_tile_off,
@@ -101,7 +108,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
                  int32_t res_levels, int32_t res_normalize,
                  const float* ca, const int32_t* seg_ca, const float* cb, const int32_t* seg_cb,
                  const float* den_in, float* den_out,
-                 int32_t* out_local, int32_t* out_global,
+                 int32_t* out_local, int32_t* out_global, int32_t screen_terms,
                  void* workspace, int64_t workspace_bytes, void* stream);
 
 /* Residual r = x - c[center_id[row]]; with normalize != 0 each dimension group

@@ -81,35 +81,57 @@ def test_nearest_forced_near_ties():
     assert got[2] == 3 and got[3] == 4 and got[4] == 11
 
 
+@pytest.mark.parametrize("terms", [1, 3])
 @pytest.mark.parametrize("xs,cs", [(1e-6, 1.0), (1.0, 1e-6), (1e-7, 1e-7), (3e3, 1.0), (1.0, 2e3)])
-def test_nearest_extreme_scales(xs, cs):
+def test_nearest_extreme_scales(xs, cs, terms):
     """Rows / centres far from unit scale: their fp16 images are mostly subnormal (flushed: the
     MFMA would otherwise align products to the subnormal's nominal exponent) or near the fp16
     range; the table scale and the measured residuals keep the screen's bound rigorous."""
     rng = np.random.default_rng(int(xs * 1e3 + cs))
-    c = (rng.standard_normal((200, 512)) * cs).astype(np.float32)
-    c[100:] *= np.float32(1e-3)                  # mixed centre norms in one table
+    c = (rng.standard_normal((128, 512)) * cs).astype(np.float32)
+    c[64:] *= np.float32(1e-3)                   # mixed centre norms in one table
     x = (rng.standard_normal((3000, 512)) * xs).astype(np.float32)
-    x[:1000] = c[rng.integers(0, 200, 1000)] + (0.05 * cs * rng.standard_normal((1000, 512))).astype(np.float32)
-    got = ops.nearest(gpu(x), ops.prepare_centers(gpu(c))).cpu().numpy()
+    x[:1000] = c[rng.integers(0, 128, 1000)] + (0.05 * cs * rng.standard_normal((1000, 512))).astype(np.float32)
+    got = ops.nearest(gpu(x), ops.prepare_centers(gpu(c)), screen_terms=terms).cpu().numpy()
     assert (got == exact_ids(x, c)).all()
 
 
 def test_prepare_centers_table_scale():
-    """c16 holds c 2^s with the largest |c 2^s| in [2^13, 2^14), no subnormals; meta = {|c|^2, |c|,
-    |c - c16 2^-s|, 2^-s}."""
+    """c16 = [hi | lo]: hi = fp16(c 2^s) with the largest |hi| in [2^13, 2^14), lo = fp16((c 2^s - hi)
+    2^12), no subnormals; meta rows {|c|^2, |c|, |2-term residual|, |1-term residual|}, row k = 2^-s."""
     rng = np.random.default_rng(5)
     c = (rng.standard_normal((300, 256)) * 3e-3).astype(np.float32)
     pc = ops.prepare_centers(gpu(c))
     meta = pc.meta.cpu().numpy()
-    h = pc.c16.cpu().numpy().view(np.float16).astype(np.float64).reshape(300, 256)
-    scale = meta[0, 3]
-    assert (meta[:, 3] == scale).all() and np.log2(scale) == np.round(np.log2(scale))
-    assert 2.0 ** 13 <= np.abs(h).max() < 2.0 ** 14
-    assert ((np.abs(h) >= 2.0 ** -14) | (h == 0)).all()
-    res = np.sqrt(((c.astype(np.float64) - h * scale) ** 2).sum(1))
-    assert np.all(meta[:, 2] >= res) and np.allclose(meta[:, 2], res, rtol=1e-6)
-    assert np.allclose(meta[:, 0], (c.astype(np.float64) ** 2).sum(1), rtol=1e-6)
+    assert meta.shape == (301, 4)
+    scale = float(meta[300, 0])
+    assert np.log2(scale) == np.round(np.log2(scale))
+    hl = pc.c16.cpu().numpy().view(np.float16).astype(np.float64)
+    hi, lo = hl[0], hl[1]
+    assert 2.0 ** 13 <= np.abs(hi).max() < 2.0 ** 14
+    for t in (hi, lo):
+        assert ((np.abs(t) >= 2.0 ** -14) | (t == 0)).all()
+    c64 = c.astype(np.float64)
+    r1 = np.sqrt(((c64 - hi * scale) ** 2).sum(1))
+    r2 = np.sqrt(((c64 - (hi + lo * 2.0 ** -12) * scale) ** 2).sum(1))
+    assert np.all(meta[:300, 3] >= r1) and np.allclose(meta[:300, 3], r1, rtol=1e-6)
+    assert np.all(meta[:300, 2] >= r2) and np.allclose(meta[:300, 2], r2, rtol=1e-6)
+    assert (r2 < r1 * 2.0 ** -9).all()
+    assert np.allclose(meta[:300, 0], (c64 ** 2).sum(1), rtol=1e-6)
+
+
+@pytest.mark.parametrize("terms", [1, 3])
+@pytest.mark.parametrize("k", [100, 128])
+def test_screen_terms_same_ids(terms, k):
+    """1- and 3-term screens return the same exact IDs (only the re-scored fraction differs)."""
+    x = synth.small_mixture(6000, d=512, m=40, seed=k)
+    c = synth.small_mixture(k, d=512, m=40, seed=k + 1)
+    ws = ops.AssignWorkspace(len(x), DEV)
+    b = ops.single_segment(len(x), DEV)
+    cand = ops.Candidates(torch.zeros(1, dtype=torch.int32, device=DEV),
+                          torch.full((1,), k, dtype=torch.int32, device=DEV), k)
+    got = ops.assign(gpu(x), ops.prepare_centers(gpu(c)), b, cand, workspace=ws, screen_terms=terms)[1]
+    assert (got.cpu().numpy() == exact_ids(x, c)).all()
 
 
 @pytest.mark.parametrize("gd,norm", [([512], True), ([128, 384], True), ([512], False), ([100, 12, 400], True)])
