@@ -25,7 +25,7 @@ def level_gaps(v, c, allowed=None):
     return top.indices[:, 0], (top.values[:, 1] - top.values[:, 0]) / scale.clamp(min=1e-30)
 
 
-ACC = ((512 // 16) * 17 + 8) * 2.0 ** -23 * 1.02
+ACC = (16 + (512 // 16) / 2 + 1) * 2.0 ** -23 * 1.02  # assign.hip accumulation_rel
 MODES = {"1term": (1, 1, 1), "xsplit": (0, 1, 1), "3term": (0, 0, 1), "3term_acc/4": (0, 0, 0.25)}
 
 

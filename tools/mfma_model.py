@@ -165,7 +165,7 @@ def main(cases=int(os.environ.get("MFMA_CASES", 40)), seed=0):
             explain(lib, *worst_case)
 
 
-if __name__ == "__main__" and not os.environ.get("MFMA_SWEEP") and not os.environ.get("MFMA_ANCHOR"):
+if __name__ == "__main__" and not (os.environ.get("MFMA_SWEEP") or os.environ.get("MFMA_ANCHOR") or os.environ.get("MFMA_TRUNC")):
     main()
 
 
@@ -236,3 +236,40 @@ def anchor_probe(lib):
 
 if __name__ == "__main__" and os.environ.get("MFMA_ANCHOR"):
     anchor_probe(_lib.load())
+
+
+def truncation_probe(lib, seed=3, trials=64):
+    """Worst truncation of the 16-product sum, in units of 2^-23 max|p|, after allowing the final
+    round-to-nearest (2^-24 |D|): one anchor product and 15 products 2^-k (k = 1..26) below it whose
+    low mantissa bits are all ones (the most a truncating aligner can drop), in every position."""
+    rng = np.random.default_rng(seed)
+    worst = 0.0
+    for trial in range(trials):
+        a = np.zeros((32, 16), np.float32)
+        b = np.zeros((16, 32), np.float32)
+        pos = rng.integers(0, 16, 32)                    # anchor position per row
+        for i in range(32):
+            for k in range(16):
+                if k == pos[i]:
+                    a[i, k] = (1 + rng.integers(0, 1024) / 1024) * rng.choice([-1, 1])
+                else:
+                    e = -int(rng.integers(1, 27))
+                    mant = 2047 if rng.random() < 0.7 else int(rng.integers(1024, 2048))
+                    a[i, k] = mant / 1024 * 2.0 ** e * (rng.choice([-1, 1]) if trial % 2 else 1)
+        b[:, :] = (1 + rng.integers(0, 1024, (16, 32)) / 1024) * (1 if trial % 4 < 2 else rng.choice([-1, 1], (16, 32)))
+        a16 = a.astype(np.float16)
+        b16 = b.astype(np.float16)
+        a16[np.abs(a16.astype(np.float32)) < 2.0 ** -14] = 0  # no subnormal operands (as the screen)
+        c = np.zeros((32, 32), np.float32)
+        d = probe(lib, a16.view(np.uint16), b16.view(np.uint16), c).astype(np.float64)
+        p = a16.astype(np.float64)[:, :, None] * b16.astype(np.float64)[None, :, :]
+        exact = p.sum(1)                                   # fp64: exact enough (span < 53 bits)
+        pmax = np.abs(p).max(1)
+        err = np.maximum(np.abs(d - exact) - 2.0 ** -24 * np.abs(d), 0)
+        worst = max(worst, float((err / (2.0 ** -23 * pmax)).max()))
+    print(f"truncation probe: worst (|D - sum p| - 2^-24 |D|) / (2^-23 max|p|) = {worst:.3f}", flush=True)
+    return worst
+
+
+if __name__ == "__main__" and os.environ.get("MFMA_TRUNC"):
+    truncation_probe(_lib.load())
