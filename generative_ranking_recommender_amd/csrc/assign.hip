@@ -32,6 +32,10 @@
 
 #include "internal.h"
 
+#ifndef RQSID_AB_MODE  // A/B timing builds only (tools/ab_build.sh): 1 no epilogue, 2 + no MFMA, 3 DMA only
+#define RQSID_AB_MODE 0
+#endif
+
 namespace rqsid {
 namespace {
 
@@ -261,7 +265,23 @@ inline float accumulation_rel(int dim) {
   return (float)((kTrunc + (dim / 16) / 2.0 + 1.0) * std::ldexp(1.0, -23) * 1.02);
 }
 
-template <int NT, int S, int RL, bool NORM, bool T3>
+// Single-pass epilogue (ONE: every segment has <= NT*32 candidates).  The per-candidate centre terms
+// collapse onto |c_k| with tile constants: |ec_k| <= gz |c_k|, |ec1_k| <= gw |c_k| (gz, gw = the largest
+// ratios over the tile's candidates, rounded up) and e0_k <= 2^-22 |c_k| ymax + 1e-30, so
+//   e_k <= A2 |c_k| + 1e-30,   A2 = A + B gz + C gw + 2.39e-7 ymax
+// and every candidate costs two packed FMAs for P = |c|^2 - 2 v.c/den and E, two packed adds for
+// ub = P + E / lb = P - E (lb overwrites the accumulator) and half a min3 (sweep 1), then a compare
+// and two selects (sweep 2: how many candidates have lb <= U, the last two of them).
+__device__ __forceinline__ float ratio_up(float num, float den) {
+  return den > 0.f ? num / den * 1.000001f : (num > 0.f ? INFINITY : 0.f);
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+template <int NT, int S, int RL, bool NORM, bool T3, bool ONE>
 __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <= 3) ? 2 : 1))) void assign_screen_kernel(AssignParams p) {
   using L = ScreenLayout<NT, S, T3>;
   constexpr int P = 4 + (NT / 2) * (T3 ? 2 : 1);  // DMA ops per wave per chunk (x: 4, centres: NT/2 per table)
@@ -352,7 +372,11 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
   const int xsw = (r >> 1) & 7;  // swizzle of this lane's row in the x image
   const int csw = (r >> 2) & 3;  // swizzle of this lane's candidate row in the centre image
 
-  const int npass = (cnt + NT * 32 - 1) / (NT * 32);
+  const int npass = ONE ? 1 : (cnt + NT * 32 - 1) / (NT * 32);
+  float* m_csq = reinterpret_cast<float*>(smem + L::kMeta);  // ONE: SoA meta |c|^2, |c|, per-wave maxima
+  float* m_y = m_csq + NT * 32;
+  float* m_red = m_y + NT * 32;
+  uint32_t pbits[ONE ? NT / 2 : 1];  // ONE: pass bits, word w = tiles 2w, 2w+1, MSB first
   for (int pass = 0; pass < npass; ++pass) {
     const int pbase = pass * NT * 32;
     // centre DMA sources: instruction j covers candidates (wave*NT/2 + j)*16 + lane/4, slot lane%4
@@ -368,7 +392,27 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
       if (T3) clo[j] = csrc[j] + (int64_t)p.n_centers * dim;
     }
     __syncthreads();
-    if (tid < NT * 32) {
+    if constexpr (ONE) {
+      float gz = 0.f, gw = 0.f, gy = 0.f;
+      if (tid < NT * 32) {
+        const bool live = pbase + tid < cnt;
+        const int kl = live ? pbase + tid : cnt - 1;
+        const float4 m = reinterpret_cast<const float4*>(p.c_meta)[cand_global(p, cbase, kl)];
+        m_csq[tid] = live ? m.x : INFINITY;
+        m_y[tid] = m.y;
+        gz = ratio_up(T3 ? m.z : m.w, m.y);
+        gw = T3 ? ratio_up(m.w, m.y) : 0.f;
+        gy = m.y;
+      }
+      gz = wave_max(gz);
+      gw = wave_max(gw);
+      gy = wave_max(gy);
+      if (lane == 0) {
+        m_red[wave * 4 + 0] = gz;
+        m_red[wave * 4 + 1] = gw;
+        m_red[wave * 4 + 2] = gy;
+      }
+    } else if (tid < NT * 32) {
       const bool live = pbase + tid < cnt;
       const int kl = live ? pbase + tid : cnt - 1;
       const float4 m = reinterpret_cast<const float4*>(p.c_meta)[cand_global(p, cbase, kl)];
@@ -405,6 +449,9 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
       }
     };
     auto compute = [&](int c) {
+#if RQSID_AB_MODE >= 3
+      return;
+#endif
       const unsigned char* xb = smem + (c % S) * L::kStage + wave * kXWaveBytes + r * 128;
       const unsigned char* cbp = smem + (c % S) * L::kStage + kXStage + r * 64;
 #pragma unroll
@@ -470,8 +517,13 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const f16x8 af = *reinterpret_cast<const f16x8*>(cbp + t * 32 * 64 + (qa << 4));
+#if RQSID_AB_MODE >= 2
+          acc[t][0] += (float)bf[0] + (float)af[0];
+          if (false) {
+#else
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[t], 0, 0, 0);
           if (T3) {
+#endif
             const f16x8 al = *reinterpret_cast<const f16x8*>(cbp + L::kCHalf + t * 32 * 64 + (qa << 4));
             accl[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bl, accl[t], 0, 0, 0);
             accl[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bf, accl[t], 0, 0, 0);
@@ -513,6 +565,18 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
       }
       vn = nrm * 1.0001f + 1e-30f;
     }
+#if RQSID_AB_MODE >= 1
+    {  // A/B timing build: no epilogue (results are wrong; tools/ab_sweep only)
+      float sink = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) sink += acc[t][v] + (T3 ? accl[t < (T3 ? NT : 1) ? t : 0][v] : 0.f);
+      if (sink == -1.2345e38f) p.out_local[my_row] = 7;
+      __syncthreads();
+      continue;
+    }
+#endif
     // epilogue.  Sweep 1: the least upper bound U over the row's candidates so far.  Sweep 2: list
     // (ascending) the candidates whose lower bound is <= U, up to kListPerHalf per lane half; U only
     // shrinks over passes, so earlier listings are re-filtered at the end.
@@ -528,6 +592,59 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
     // the MFMA sums are in units of 2^s of the centre table (rqsid_prepare_centers; exact power of two)
     const float m2 = -2.0f * inv_den *
                      __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(p.c_meta[4 * p.n_centers])));
+    if constexpr (ONE) {
+      float gz = 0.f, gw = 0.f, gy = 0.f;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        gz = fmaxf(gz, m_red[w * 4 + 0]);
+        gw = fmaxf(gw, m_red[w * 4 + 1]);
+        gy = fmaxf(gy, m_red[w * 4 + 2]);
+      }
+      const float A2 = (A + B * gz + C * gw + 2.39e-7f * gy) * 1.000001f;
+      const f2 m2v = {m2, m2}, a2v = {A2, A2}, epsv = {1e-30f, 1e-30f};
+      // sweep 1: ub / lb per candidate (lb kept in the accumulator), U = least ub
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 cs = *reinterpret_cast<const float4*>(m_csq + t * 32 + 8 * g + 4 * h);
+          const float4 yy = *reinterpret_cast<const float4*>(m_y + t * 32 + 8 * g + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int v = 4 * g + 2 * e;
+            f2 d = {acc[t][v], acc[t][v + 1]};
+            if (T3) d = f2{accl[T3 ? t : 0][v], accl[T3 ? t : 0][v + 1]} * 0x1p-12f + d;
+            const f2 P = m2v * d + (e ? f2{cs.z, cs.w} : f2{cs.x, cs.y});
+            const f2 E = a2v * (e ? f2{yy.z, yy.w} : f2{yy.x, yy.y}) + epsv;
+            const f2 ub = P + E, lb = P - E;
+            U = fminf(U, fminf(ub.x, ub.y));
+            acc[t][v] = lb.x;
+            acc[t][v + 1] = lb.y;
+          }
+        }
+      }
+      U = fminf(U, __shfl_xor(U, 32));
+      // sweep 2: one bit per candidate, lb <= U, i.e. the sign of lb - Up with Up > U by >= 2 ulp (a
+      // candidate admitted by rounding is only re-scored); v_alignbit shifts the sign into the word.
+      // v = 0..15 is ascending in candidate order, so word w holds tile 2w's candidates from bit 31
+      // down, then tile 2w+1's.
+      const float Up = fmaf(fabsf(U), 0x1p-22f, U) + 1.2e-38f;
+      const f2 upv = {Up, Up};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t b = (t & 1) ? pbits[t >> 1] : 0u;
+#pragma unroll
+        for (int v = 0; v < 16; v += 2) {
+          const f2 d = f2{acc[t][v], acc[t][v + 1]} - upv;
+          b = __builtin_amdgcn_alignbit(b, __float_as_uint(d.x), 31);
+          b = __builtin_amdgcn_alignbit(b, __float_as_uint(d.y), 31);
+        }
+        pbits[t >> 1] = b;
+      }
+      continue;  // npass == 1
+    }
     const float4* meta = lds_meta + 4 * h;
     const int kl_h = pbase + 4 * h;
     // sweep 1: U = least upper bound.  The scheduling barriers stop hipcc from hoisting every
@@ -572,6 +689,79 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
     __syncthreads();  // meta / ring are rewritten by the next pass
   }
 
+#if RQSID_AB_MODE >= 1
+  if (h == 0 && row_valid) {  // hashed ids keep the next level's segment mix realistic
+    const int k = (int)(((uint32_t)my_row * 2654435761u) >> 8) % cnt;
+    p.out_local[my_row] = cand_local(p, cbase, k);
+    p.out_global[my_row] = cand_global(p, cbase, k);
+  }
+  return;
+#endif
+  if constexpr (ONE) {
+    // decode up to kListPerHalf passing candidates of this lane half, ascending: bit 31-j of word w
+    // is tile 2w + j/16, value v = j%16, candidate t*32 + (v&3) + 8(v>>2) + 4h
+    int pc = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 2; ++w) pc += __popc(pbits[w]);
+    int kk[kListPerHalf];
+#pragma unroll
+    for (int j = 0; j < kListPerHalf; ++j) kk[j] = -1;
+    int n = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 2; ++w) {
+      uint32_t b = pbits[w];
+#pragma unroll
+      for (int x = 0; x < kListPerHalf; ++x) {  // the first set bits of word w, in order
+        const int jj = __clz(b);
+        const int t = 2 * w + (jj >> 4), v = jj & 15;
+        const int k = t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        const bool got = b != 0;
+#pragma unroll
+        for (int j = 0; j < kListPerHalf; ++j) kk[j] = got && n == j ? k : kk[j];
+        n += got ? 1 : 0;
+        b = got ? b & ~(0x80000000u >> jj) : b;
+      }
+    }
+    const int pc_o = __shfl_xor(pc, 32);
+    int kp[kListPerHalf];
+#pragma unroll
+    for (int j = 0; j < kListPerHalf; ++j) kp[j] = __shfl_xor(kk[j], 32);
+    const int ncand = pc + pc_o;
+    const bool overflow = pc > kListPerHalf || pc_o > kListPerHalf || ncand == 0;
+    const bool definitive = !overflow && ncand == 1;
+    if (h == 0 && row_valid && definitive) {
+      const int k = max(kk[0], kp[0]);
+      p.out_local[my_row] = cand_local(p, cbase, k);
+      p.out_global[my_row] = cand_global(p, cbase, k);
+    }
+    WorkItem w{};
+    w.row = my_row;
+    w.seg = s;
+    if (overflow) {
+      w.n = -1;
+    } else {
+      // merge the two ascending half lists (empty slots last)
+      int c8[kMaxList];
+#pragma unroll
+      for (int j = 0; j < kListPerHalf; ++j) {
+        c8[j] = kk[j] >= 0 ? kk[j] : INT_MAX;
+        c8[kListPerHalf + j] = kp[j] >= 0 ? kp[j] : INT_MAX;
+      }
+#pragma unroll
+      for (int i = 0; i < kMaxList; ++i)
+#pragma unroll
+        for (int j = 0; j < kMaxList - 1 - i; ++j) {
+          const int a = c8[j], bq = c8[j + 1];
+          c8[j] = min(a, bq);
+          c8[j + 1] = max(a, bq);
+        }
+#pragma unroll
+      for (int j = 0; j < kMaxList; ++j) w.cand[j] = (uint16_t)(c8[j] == INT_MAX ? 0xFFFF : c8[j]);
+      w.n = ncand;
+    }
+    push_work(p, h == 0 && row_valid && !definitive, lane, w);
+    return;
+  }
   // Row decision: keep the listed candidates still within the final U; a half that listed more
   // than kListPerHalf overflows -> re-score every candidate of the segment.
   bool ovf = nlist > kListPerHalf || cnt > 65535;
@@ -814,19 +1004,19 @@ __global__ __launch_bounds__(64) void mfma_probe_kernel(const uint16_t* __restri
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-template <int NT, int S, bool T3>
+template <int NT, int S, bool T3, bool ONE>
 void set_attrs(bool* ok) {
   const int bytes = ScreenLayout<NT, S, T3>::kMaxBytes;
-  const void* ks[] = {(const void*)assign_screen_kernel<NT, S, 0, false, T3>,
-                      (const void*)assign_screen_kernel<NT, S, 1, false, T3>,
-                      (const void*)assign_screen_kernel<NT, S, 1, true, T3>,
-                      (const void*)assign_screen_kernel<NT, S, 2, false, T3>,
-                      (const void*)assign_screen_kernel<NT, S, 2, true, T3>};
+  const void* ks[] = {(const void*)assign_screen_kernel<NT, S, 0, false, T3, ONE>,
+                      (const void*)assign_screen_kernel<NT, S, 1, false, T3, ONE>,
+                      (const void*)assign_screen_kernel<NT, S, 1, true, T3, ONE>,
+                      (const void*)assign_screen_kernel<NT, S, 2, false, T3, ONE>,
+                      (const void*)assign_screen_kernel<NT, S, 2, true, T3, ONE>};
   for (const void* k : ks)
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) *ok = false;
 }
 
-// ring-depth variant (tuning experiments): 0 (default) S=2; 1: NT4 S6 / NT8 S3; 3: NT4 S3 / NT8 S4
+// screen variant (tuning experiments): 0 default; 2: multi-sweep list epilogue on single-pass segments
 int screen_variant() {
   static int v = [] {
     const char* e = getenv("RQSID_SCREEN_VARIANT");
@@ -839,27 +1029,30 @@ bool g_attr_done = false;
 int ensure_attrs() {
   if (g_attr_done) return RQSID_OK;
   bool ok = true;
-  set_attrs<4, 3, false>(&ok);
-  set_attrs<4, 6, false>(&ok);
-  set_attrs<8, 4, false>(&ok);
-  set_attrs<8, 3, false>(&ok);
-  set_attrs<4, 2, false>(&ok);
-  set_attrs<8, 2, false>(&ok);
-  set_attrs<4, 2, true>(&ok);
-  set_attrs<4, 3, true>(&ok);
+  set_attrs<4, 2, false, true>(&ok);
+  set_attrs<8, 2, false, true>(&ok);
+  set_attrs<4, 2, true, true>(&ok);
+  set_attrs<4, 2, false, false>(&ok);
+  set_attrs<8, 2, false, false>(&ok);
+  set_attrs<4, 2, true, false>(&ok);
   if (!ok) return fail(RQSID_E_LAUNCH, "assign: cannot raise the dynamic LDS limit");
   g_attr_done = true;
   return RQSID_OK;
 }
 
-template <int NT, int S, bool T3>
+template <int NT, int S, bool T3, bool ONE>
 void launch_screen(const AssignParams& p, int rl, bool norm, unsigned grid, hipStream_t st) {
   const size_t lds = ScreenLayout<NT, S, T3>::bytes(rl, p.dim);
-  if (rl == 0) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 0, false, T3>), dim3(grid), dim3(256), lds, st, p);
-  else if (rl == 1 && norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, true, T3>), dim3(grid), dim3(256), lds, st, p);
-  else if (rl == 1) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, false, T3>), dim3(grid), dim3(256), lds, st, p);
-  else if (norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, true, T3>), dim3(grid), dim3(256), lds, st, p);
-  else hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, false, T3>), dim3(grid), dim3(256), lds, st, p);
+  if (rl == 0) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 0, false, T3, ONE>), dim3(grid), dim3(256), lds, st, p);
+  else if (rl == 1 && norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, true, T3, ONE>), dim3(grid), dim3(256), lds, st, p);
+  else if (rl == 1) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, false, T3, ONE>), dim3(grid), dim3(256), lds, st, p);
+  else if (norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, true, T3, ONE>), dim3(grid), dim3(256), lds, st, p);
+  else hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, false, T3, ONE>), dim3(grid), dim3(256), lds, st, p);
+}
+template <int NT, int S, bool T3>
+void launch_screen2(const AssignParams& p, int rl, bool norm, unsigned grid, bool one, hipStream_t st) {
+  if (one) launch_screen<NT, S, T3, true>(p, rl, norm, grid, st);
+  else launch_screen<NT, S, T3, false>(p, rl, norm, grid, st);
 }
 
 }  // namespace
@@ -953,22 +1146,16 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   // Terms: the 3-term screen (rounding residuals of both operands summed by two more MFMAs) shrinks
   // the bound ~5x at 2 blocks/CU; auto picks it for residual levels with <= 128 candidates, where
   // trained codebooks leave the most rows inside the 1-term bound ("Screen terms").
-  const int v = screen_variant();
   // (The 8-tile form has no 3-term build: its second accumulator set does not fit 256 VGPRs.)
+  // ONE: single-pass segments take the collapsed-bound epilogue (RQSID_SCREEN_VARIANT=2: the
+  // per-candidate two-sweep list epilogue, for comparison).
   const bool t3 = cand_count_max <= 128 && (screen_terms == 3 || (screen_terms == 0 && res_levels >= 1));
   p.terms = t3 ? 3 : 1;
-  if (t3) {
-    if (v == 3) launch_screen<4, 3, true>(p, res_levels, norm, grid, st);
-    else launch_screen<4, 2, true>(p, res_levels, norm, grid, st);
-  } else if (cand_count_max <= 128) {
-    if (v == 1) launch_screen<4, 6, false>(p, res_levels, norm, grid, st);
-    else if (v == 3) launch_screen<4, 3, false>(p, res_levels, norm, grid, st);
-    else launch_screen<4, 2, false>(p, res_levels, norm, grid, st);
-  } else {
-    if (v == 1) launch_screen<8, 3, false>(p, res_levels, norm, grid, st);
-    else if (v == 3) launch_screen<8, 4, false>(p, res_levels, norm, grid, st);
-    else launch_screen<8, 2, false>(p, res_levels, norm, grid, st);
-  }
+  const bool legacy = screen_variant() == 2;
+  if (t3) launch_screen2<4, 2, true>(p, res_levels, norm, grid, !legacy, st);
+  else if (cand_count_max <= 128) launch_screen2<4, 2, false>(p, res_levels, norm, grid, !legacy, st);
+  else if (cand_count_max <= 256) launch_screen2<8, 2, false>(p, res_levels, norm, grid, !legacy, st);
+  else launch_screen<8, 2, false, false>(p, res_levels, norm, grid, st);
   if ((rc = check_launch("assign_screen"))) return rc;
   const dim3 g(4096);  // multiple of 8 (XCD-grouped work runs)
   if (res_levels == 0) hipLaunchKernelGGL((assign_rescore_kernel<0, false>), g, dim3(256), 0, st, p);

@@ -60,6 +60,20 @@ def emulated_ambiguous(v_pre, c, allowed=None):
             lb = torch.where(allowed, lb, torch.full_like(lb, float("inf")))
         U = ub.min(1, keepdim=True).values
         out[name] = ((lb <= U).sum(1) > 1).double().sum().item()
+        # loose epilogue: one per-row bound Emax = A max|c| + B max|ec| over the allowed set;
+        # pass iff sc <= min sc + 2 Emax (the cheap count test), and the pass-count histogram
+        cn = cd.norm(dim=1)[None, :].expand_as(sc)
+        ecn = ec[None, :].expand_as(sc)
+        if allowed is not None:
+            cn = torch.where(allowed, cn, torch.zeros_like(cn))
+            ecn = torch.where(allowed, ecn, torch.zeros_like(ecn))
+            scm = torch.where(allowed, sc, torch.full_like(sc, float("inf")))
+        else:
+            scm = sc
+        emax = A * cn.max(1).values + B * ecn.max(1).values
+        npass = (scm <= scm.min(1).values[:, None] + 2.0 * emax[:, None]).sum(1)
+        out[name + "_loose"] = (npass > 1).double().sum().item()
+        out[name + "_loose_ovf8"] = (npass > 8).double().sum().item()
     return out
 
 
@@ -69,7 +83,13 @@ def normalize(r):
 
 def main(n=int(os.environ.get("GAP_ROWS", 100_000))):
     dev = torch.device("cuda", 0)
-    cb = bench.codebooks(os.environ.get("BENCH_CODEBOOKS", "fitted"), dev)
+    cache = os.environ.get("SWEEP_CB")
+    if cache and os.path.exists(cache):
+        import numpy as np
+        z = np.load(cache)
+        cb = {k: z[k] for k in z.files}
+    else:
+        cb = bench.codebooks(os.environ.get("BENCH_CODEBOOKS", "fitted"), dev)
     c0, c1, c2 = (torch.from_numpy(cb[k]).to(dev) for k in ("c0", "c1", "c2"))
     match = torch.from_numpy(cb["match"]).to(dev).bool()
     x = bench.make_rows(n, 0, dev)
@@ -84,18 +104,20 @@ def main(n=int(os.environ.get("GAP_ROWS", 100_000))):
             a1[m], g1[m] = i + p * 128, g
     r2 = normalize(r1 - c1[a1])
     a2, g2 = level_gaps(r2, c2, match[a1])
-    amb1 = {k: 0.0 for k in MODES}
+    keys = [k + suf for k in MODES for suf in ("", "_loose", "_loose_ovf8")]
+    amb1 = {k: 0.0 for k in keys}
     for p in range(c0.shape[0]):
         m = a0 == p
         if m.any():
             for k, v in emulated_ambiguous(x[m] - c0[p], c1[p * 128:(p + 1) * 128]).items():
                 amb1[k] += v
-    amb2 = {k: 0.0 for k in MODES}
+    amb0 = emulated_ambiguous(x, c0)
+    amb2 = {k: 0.0 for k in keys}
     for i in range(0, n, 20000):
         for k, v in emulated_ambiguous(r1[i:i + 20000] - c1[a1[i:i + 20000]], c2, match[a1[i:i + 20000]]).items():
             amb2[k] += v
-    for k in MODES:
-        print(f"emulated ambiguity [{k}]: L1 {amb1[k] / n:.4f} L2 {amb2[k] / n:.4f}", flush=True)
+    for k in keys:
+        print(f"emulated ambiguity [{k}]: L0 {amb0[k] / n:.4f} L1 {amb1[k] / n:.4f} L2 {amb2[k] / n:.4f}", flush=True)
     for lvl, g in enumerate((g0, g1, g2)):
         print(f"L{lvl}: median gap {g.median().item():.3e}  " +
               " ".join(f"<{t:.0e}:{(g < t).double().mean().item():.4f}" for t in THR), flush=True)

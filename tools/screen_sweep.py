@@ -5,6 +5,7 @@ import os
 import sys
 from pathlib import Path
 
+import numpy as np
 import torch
 
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
@@ -16,7 +17,14 @@ from generative_ranking_recommender_amd.encode import HIERARCHICAL_TRAIN, RQEnco
 
 def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000)), reps=int(os.environ.get("SWEEP_REPS", 5))):
     dev = torch.device("cuda", 0)
-    cb = bench.codebooks(os.environ.get("BENCH_CODEBOOKS", "fitted"), dev)
+    cache = os.environ.get("SWEEP_CB")  # codebooks fitted once with the real library (A/B builds reuse them)
+    if cache and os.path.exists(cache):
+        z = np.load(cache)
+        cb = {k: z[k] for k in z.files}
+    else:
+        cb = bench.codebooks(os.environ.get("BENCH_CODEBOOKS", "fitted"), dev)
+        if cache:
+            np.savez(cache, **cb)
     enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], [128, 128, 256],
                     match=torch.from_numpy(cb["match"]), semantics=HIERARCHICAL_TRAIN, device=dev)
     x = bench.make_rows(n, 0, dev)
@@ -41,7 +49,7 @@ def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000)), reps=int(os.environ.ge
     e.record()
     torch.cuda.synchronize()
     ms = timer.mean_ms()
-    print(f"variant={os.environ.get('RQSID_SCREEN_VARIANT', '0')} step={s.elapsed_time(e) / reps:.2f} ms " +
+    print(f"lib={os.environ.get('RQSID_LIB', 'default')} variant={os.environ.get('RQSID_SCREEN_VARIANT', '0')} step={s.elapsed_time(e) / reps:.2f} ms " +
           " ".join(f"{k}={v:.3f}" for k, v in sorted(ms.items())), flush=True)
 
 
