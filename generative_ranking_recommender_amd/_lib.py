@@ -15,8 +15,9 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 REPO = PKG.parent
 LIB_PATH = PKG / "librqsid.so"
-SRCS = [PKG / "csrc" / "rqsid.hip", PKG / "csrc" / "assign.hip", PKG / "csrc" / "auction.hip"]
-DEPS = SRCS + [PKG / "csrc" / "internal.h"]
+SRCS = [PKG / "csrc" / "rqsid.hip", PKG / "csrc" / "assign.hip", PKG / "csrc" / "assign_stream.hip",
+        PKG / "csrc" / "auction.hip"]
+DEPS = SRCS + [PKG / "csrc" / "internal.h", PKG / "csrc" / "assign_common.h"]
 HEADER = REPO / "include" / "rqsid.h"
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC"]

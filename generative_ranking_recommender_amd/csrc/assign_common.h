@@ -1,0 +1,283 @@
+// assign_common.h — definitions shared by the screening kernels (assign.hip: per-tile kernel for any
+// shape; assign_stream.hip: the persistent streamed kernel for single-pass segments).  Not ABI.
+#pragma once
+#include <cmath>
+#include <cstdlib>
+
+#include "internal.h"
+
+#ifndef RQSID_AB_MODE  // A/B timing builds only (tools/ab_build.sh): 1 no epilogue, 2 + no MFMA, 3 DMA only
+#define RQSID_AB_MODE 0
+#endif
+
+namespace rqsid {
+
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(2))) _Float16 h2;
+typedef __attribute__((ext_vector_type(2))) float f2;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int kWaves = 4;
+constexpr int kRowsPerWave = 32;
+constexpr int kTileRows = kWaves * kRowsPerWave;  // rows per work tile
+constexpr int kChunk = 32;                         // dims per ring stage
+constexpr int kXWaveBytes = kRowsPerWave * 128;    // 4 KiB: 32 rows x 32 fp32 dims
+constexpr int kXStage = kWaves * kXWaveBytes;      // 16 KiB
+constexpr int kMaxDim = 1024;
+
+constexpr int kListPerHalf = 4;             // candidates a lane half can list exactly
+constexpr int kMaxList = 2 * kListPerHalf;   // per row
+struct WorkItem {
+  int32_t row;
+  int32_t seg;
+  int32_t n;  // >=1: explicit local candidates in cand[]; -1: every candidate; -2: penalty (all centres); -3: none
+  int32_t pad;
+  uint16_t cand[kMaxList];
+};
+static_assert(sizeof(WorkItem) == 32, "work item layout");
+
+struct AssignParams {
+  const float* x;
+  int32_t dim;
+  const int32_t* row_index;
+  int32_t n_segments;
+  const int32_t* seg_row_off;
+  const int32_t* seg_tile_off;
+  const float* centers;
+  const uint16_t* c16;   // fp16 bits [2][k][dim]: hi, lo tables (rqsid_prepare_centers)
+  const float* c_meta;   // [k+1] float4: per centre |c|^2, |c|, |c - (hi + lo 2^-12) 2^-s|, |c - hi 2^-s|; row k: 2^-s
+  int32_t n_centers;
+  const int32_t* cand_base;
+  const int32_t* cand_count;
+  const int32_t* cand_idx;
+  const int32_t* cand_lid;  // local id reported for list position j (NULL: j)
+  const uint8_t* seg_flags;
+  int32_t* out_local;
+  int32_t* out_global;
+  WorkItem* work;
+  int32_t* work_count;
+  const int32_t* work_idx;  // NULL: work[] is the compact list; else the list is work[work_idx[i]]
+  int64_t work_cap;
+  float acc_rel;
+  int32_t terms;          // 1 or 3 (screen product terms; host-side dispatch only)
+  const float* ca;
+  const int32_t* seg_ca;
+  const float* cb;
+  const int32_t* seg_cb;
+  const float* den_in;
+  float* den_out;
+};
+
+__device__ __forceinline__ int cand_global(const AssignParams& p, int base, int local) {
+  return p.cand_idx ? p.cand_idx[base + local] : base + local;
+}
+__device__ __forceinline__ int cand_local(const AssignParams& p, int base, int pos) {
+  return p.cand_lid ? p.cand_lid[base + pos] : pos;
+}
+__device__ __forceinline__ int seg_row(const int32_t* map, int s) { return map ? map[s] : s; }
+
+// fp16 centre operand with a rigorous residual.  The MFMA aligns its 16 products to the largest
+// NOMINAL exponent, and a subnormal fp16 operand counts as exponent -14 whatever its value
+// (tools/mfma_model.py anchor_probe: 2^-24 x 2^10 truncates its neighbours like a 2^-4 product
+// would), so no subnormal may reach it: the centre table is scaled by a power of two 2^s that puts
+// its largest element just below 2^14, and scaled values below the fp16 normal range go in as 0
+// (their value lands in the measured |c - c16|).  Rows get the same treatment from the MODE
+// register (assign_screen_kernel).
+__device__ __forceinline__ _Float16 to_f16(float v) {
+  const float a = fabsf(v);
+  return (_Float16)((a >= 0x1p-14f && a < 65504.0f) ? v : 0.0f);
+}
+
+// table scale exponent: max |c| 2^s < 2^14 (s = 0 for an empty / all-zero / non-finite table)
+__device__ __forceinline__ int table_scale_exp(unsigned maxbits) {
+  const float m = __uint_as_float(maxbits);
+  if (!(m > 0.f) || !(m <= 3.4e38f)) return 0;
+  int e;
+  frexpf(m, &e);  // m < 2^e
+  return min(max(14 - e, -100), 100);
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lds_addr(const void* ptr) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)ptr;
+}
+
+// One global_load_lds_dwordx4: every lane moves 16 B from its own global address to
+// lds_base + lane*16.  Inline asm keeps hipcc's waitcnt pass from draining the ring.
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+// with an immediate byte offset (13-bit signed).  NOTE: the offset moves BOTH addresses: the LDS
+// destination is M0 + OFF + 16 lane, so pass lds_base = (wanted destination) - OFF.
+template <int OFF>
+__device__ __forceinline__ void dma16_off(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off offset:%3\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base), "i"(OFF)
+      : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void dma16_nt_off(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off offset:%3 nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base), "i"(OFF)
+      : "memory");
+}
+// The same with the non-temporal hint, for the once-read row stream: rows then do not displace
+// the centre tables every tile re-reads from L2 (tools/probe/dma_probe2.hip: 4.4 -> 4.7 TB/s at 2
+// blocks/CU with a 256-candidate centre stream, 6.2 -> 6.7 TB/s rows alone).
+__device__ __forceinline__ void dma16_nt(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+// wait until at most N of this wave's vector-memory ops are outstanding, drain LDS ops, barrier
+template <int N>
+__device__ __forceinline__ void wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
+}
+
+template <int S, int P>
+__device__ __forceinline__ void wait_chunks(int younger) {
+  // younger = chunks issued after the one we need (uniform, <= S-2); each chunk is P DMA ops per wave
+  static_assert((S - 2) * P <= 63, "vmcnt field is 6 bits");
+  if (S >= 7 && younger >= 5) wait_barrier<(S >= 7 ? 5 * P : 0)>();
+  else if (S >= 6 && younger >= 4) wait_barrier<(S >= 6 ? 4 * P : 0)>();
+  else if (S >= 5 && younger >= 3) wait_barrier<(S >= 5 ? 3 * P : 0)>();
+  else if (S >= 4 && younger >= 2) wait_barrier<(S >= 4 ? 2 * P : 0)>();
+  else if (younger >= 1) wait_barrier<P>();
+  else wait_barrier<0>();
+}
+
+__device__ __forceinline__ void push_work(const AssignParams& p, bool need, int lane, const WorkItem& w) {
+  const unsigned long long m = __ballot(need);
+  if (!m) return;
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(p.work_count, __popcll(m));
+  base = __shfl(base, leader);
+  if (need) {
+    const int idx = base + __popcll(m & ((1ull << lane) - 1ull));
+    if (idx < p.work_cap) p.work[idx] = w;
+  }
+}
+
+constexpr double kTrunc = 16.0;  // per-instruction truncation allowance (8x the worst observed)
+inline float accumulation_rel(int dim) {
+  return (float)((kTrunc + (dim / 16) / 2.0 + 1.0) * std::ldexp(1.0, -23) * 1.02);
+}
+
+// Pass-bit decoding of the single-pass screens: word w holds tiles 2w, 2w+1 (bit 31-j: tile
+// 2w + j/16, value j%16, candidate t*32 + (j&3) + 8((j&15)>>2) + 4h; ascending from the MSB of word 0).
+// Returns the lowest passing candidate of this lane half and clears its bit (-1 if none).
+template <int NW>
+__device__ __forceinline__ int pass_take_first(uint32_t (&wv)[NW], int h) {
+  int ws = -1;
+  uint32_t b = 0;
+#pragma unroll
+  for (int w = NW - 1; w >= 0; --w) {
+    const bool nz = wv[w] != 0;
+    ws = nz ? w : ws;
+    b = nz ? wv[w] : b;
+  }
+  const int jj = __clz(b) & 31;
+  const int t = 2 * ws + (jj >> 4), v = jj & 15;
+  const int k = ws >= 0 ? t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h : -1;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) wv[w] = w == ws ? (wv[w] & ~(0x80000000u >> jj)) : wv[w];
+  return k;
+}
+
+// Row decision of the single-pass screens from the pass bits of both lane halves (lanes l, l^32 hold
+// the same row).  definitive: exactly one candidate passed (k_out); else the work item lists the
+// (<= kListPerHalf per half, ascending) passing candidates or -1 (re-score every candidate).  The
+// list is built only in waves where some row needs one (the common row costs one extraction).
+template <int NW>
+__device__ __forceinline__ bool pass_decide(const uint32_t (&pbits)[NW], int h, int& k_out, WorkItem& w) {
+  int pc = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) pc += __popc(pbits[i]);
+  const int pc_o = __shfl_xor(pc, 32);
+  const int ncand = pc + pc_o;
+  const bool overflow = pc > kListPerHalf || pc_o > kListPerHalf || ncand == 0;
+  const bool definitive = !overflow && ncand == 1;
+  uint32_t wv[NW];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) wv[i] = pbits[i];
+  const int k0 = pass_take_first(wv, h);
+  k_out = max(k0, __shfl_xor(k0, 32));
+  w.n = overflow ? -1 : ncand;
+  if (__builtin_amdgcn_ballot_w64(!definitive && !overflow)) {  // wave-uniform: some row needs a list
+    int kk[kListPerHalf];
+    kk[0] = k0;
+#pragma unroll
+    for (int j = 1; j < kListPerHalf; ++j) kk[j] = pass_take_first(wv, h);
+    int c8[kMaxList];
+#pragma unroll
+    for (int j = 0; j < kListPerHalf; ++j) {
+      const int o = __shfl_xor(kk[j], 32);
+      c8[j] = kk[j] >= 0 ? kk[j] : INT_MAX;
+      c8[kListPerHalf + j] = o >= 0 ? o : INT_MAX;
+    }
+#pragma unroll
+    for (int i = 0; i < kMaxList; ++i)
+#pragma unroll
+      for (int j = 0; j < kMaxList - 1 - i; ++j) {
+        const int a = c8[j], bq = c8[j + 1];
+        c8[j] = min(a, bq);
+        c8[j + 1] = max(a, bq);
+      }
+#pragma unroll
+    for (int j = 0; j < kMaxList; ++j) w.cand[j] = (uint16_t)(c8[j] == INT_MAX ? 0xFFFF : c8[j]);
+  }
+  return definitive;
+}
+
+__device__ __forceinline__ float ratio_up(float num, float den) {
+  return den > 0.f ? num / den * 1.000001f : (num > 0.f ? INFINITY : 0.f);
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+
+// table-wide epilogue constants written by rqsid_prepare_centers into meta row k:
+// {2^-s, max |ec2|/|c|, max |ec1|/|c|, max |c|} (rounded up)
+void launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
+                          int32_t* seg_tile256, int64_t cap, hipStream_t st);
+bool stream_supported(int nt, bool t3, int rl, bool norm);
+
+}  // namespace rqsid

@@ -1,0 +1,644 @@
+// assign_stream.hip — the persistent, cross-tile pipelined screening kernel (rqsid_assign's fast path
+// for single-pass segments of 512-d rows: every segment has <= NT*32 candidates).
+//
+// Same arithmetic as assign.hip's assign_screen_kernel<..., ONE = true> (fp16 MFMA screen, the
+// collapsed per-candidate bound, pass bit masks, fp64 re-score of ambiguous rows), different data
+// movement:
+//  * One persistent 8-wave block per CU walks an XCD-contiguous run of 256-row tiles (twice the
+//    rows per centre image of the per-tile kernel: the centre stream costs HBM-side bandwidth, see
+//    tools/probe/dma_probe2.hip).  The LDS-DMA ring (kSS = 3 stages of 32-dim chunks: x 32 KiB with
+//    the non-temporal hint + centres 2*NT KiB [+ lo 2*NT KiB]) never drains at a tile boundary: the
+//    last two chunk slots of tile j already stream tile j+1's first chunks, so tile j's epilogue
+//    (VALU only) overlaps tile j+1's HBM traffic.
+//  * Tile j+1's header is fetched during tile j in two DMA levels (row / candidate indices and the
+//    residual centre rows; then the candidates' |c|^2, |c| and the rows' den_in), counted on the same
+//    vmcnt as the ring (every wait below is a counted vmcnt(N) for the exact number of younger ops).
+//  * Outputs are written by a FIXED number of stores per wave (out_local, out_global [, den_out];
+//    dummy targets for inactive lanes) so the next tile's counted waits stay exact; rows that need
+//    the fp64 re-score get out_global = -2 and their work item at work[row] (a conditional store can
+//    only make a later counted wait stronger, never weaker); a compaction pass lists them.
+#include "assign_common.h"
+
+namespace rqsid {
+namespace {
+
+constexpr int kSS = 3;                    // ring stages
+constexpr int kSC = 32;                   // dims per chunk (128-B row pieces: gathered rows stream at full rate)
+constexpr int kSDim = 512;                // the stream kernel's row width
+constexpr int kNch = kSDim / kSC;         // chunks per tile
+constexpr int kSW = 8;                    // waves per block
+constexpr int kSR = kSW * 32;             // rows per tile
+constexpr int kSX = kSR * kSC * 4;        // x stage: 256 rows x 128 B
+constexpr int kSentinel = -2;             // out_global of a row left to the re-score
+
+template <int NT, int RL, bool NORM, bool T3>
+struct StreamLayout {
+  static constexpr int kCen = NT * 32 * kSC * 2;  // one fp16 centre table image: NT*32 x 64 B
+  static constexpr int kStage = kSX + kCen * (T3 ? 2 : 1);
+  static constexpr int kRes = kSS * kStage;                    // [2 parities][RL rows] fp32 512
+  static constexpr int kSoa = kRes + 2 * RL * kSDim * 4;        // [2 parities][csq | y][NT*32] f32
+  static constexpr int kCidx = kSoa + 2 * 2 * NT * 32 * 4;      // [2 parities][NT*32] i32
+  static constexpr int kLand = kCidx + 2 * NT * 32 * 4;         // [8 waves][32] i32 (row idx, then den)
+  static constexpr int kBytes = kLand + kSW * 32 * 4;
+  static constexpr int P = 4 + (NT / 4) * (T3 ? 2 : 1);        // ring DMA ops per chunk per wave
+  static constexpr int E = 2 + (RL == 1 && NORM ? 1 : 0);       // fixed epilogue stores per wave
+  static constexpr int H1 = 2 + (RL >= 1 ? 1 : 0);              // header level-1 DMA ops per wave
+  static constexpr int H2 = 2 + (RL == 2 ? 1 : 0);              // header level-2 DMA ops per wave
+  static_assert(2 * P + E + H1 + H2 <= 63, "vmcnt field is 6 bits");
+};
+
+// one global_load_lds_dword: every lane moves 4 B from its own address to lds_base + lane*4
+__device__ __forceinline__ void dma4(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+// s_load_dword issued from asm: an SMEM load (lgkmcnt), invisible to hipcc's vmcnt bookkeeping and
+// never turned into a vector load.  The value is read only after a later wait_barrier (its
+// lgkmcnt(0)) and an SGPR_PIN.
+__device__ __forceinline__ int sload(const void* ptr) {
+  const uint64_t a = reinterpret_cast<uint64_t>(ptr);  // uniform by construction; say so to hipcc
+  const uint64_t u = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+  int v;
+  asm volatile("s_load_dword %0, %1, 0x0" : "=s"(v) : "s"(u) : "memory");
+  return v;
+}
+// (a macro, not a function taking int&: through a reference hipcc loses track of the SGPR)
+#define SGPR_PIN(v) asm volatile("" : "+s"(v))
+
+struct TileHdr {  // block-uniform (SGPRs)
+  int T, s, t0, nrows, cnt, cbase, ca_row, cb_row;
+  bool pen;   // penalty segment or no candidates: no screen, work items only
+  bool flag;  // RQSID_SEG_PENALTY
+};
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ TileHdr tile_header(const AssignParams& p, const int32_t* tile_seg,
+                                               const int32_t* seg_tile256, int T) {
+  TileHdr H;
+  H.T = T;
+  H.s = uni(tile_seg[T]);
+  const int s = H.s;
+  const int r0 = uni(p.seg_row_off[s]), r1 = uni(p.seg_row_off[s + 1]), tb = uni(seg_tile256[s]);
+  H.t0 = r0 + (T - tb) * kSR;
+  H.nrows = min(kSR, r1 - H.t0);
+  H.cnt = uni(p.cand_count[s]);
+  H.cbase = uni(p.cand_base[s]);
+  H.flag = p.seg_flags && (uni(p.seg_flags[s]) & RQSID_SEG_PENALTY);
+  H.pen = H.flag || H.cnt <= 0;
+  H.ca_row = p.seg_ca ? uni(p.seg_ca[s]) : s;
+  H.cb_row = p.seg_cb ? uni(p.seg_cb[s]) : s;
+  return H;
+}
+
+template <int NT, int RL, bool NORM, bool T3>
+__global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, const int32_t* tile_seg,
+                                                              const int32_t* seg_tile256) {
+  using L = StreamLayout<NT, RL, NORM, T3>;
+  constexpr int P = L::P;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#ifndef RQSID_AB_NO_FLUSH
+  asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 6, 2), 0");  // fp16/fp64 denormals flushed (to_f16)
+#endif
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = uni(tid >> 6);
+  const int h = lane >> 5, r = lane & 31;
+  const uint32_t lds0 = lds_addr(smem);
+
+  // XCD-contiguous tile runs: block b runs on XCD b % 8; the G/8 blocks of an XCD walk one eighth of
+  // the tile space together, so a segment's tiles (and its candidate centres) stay in one L2.
+  const int ntiles = uni(seg_tile256[p.n_segments]);
+  const int G8 = (int)(gridDim.x >> 3), xcd = (int)(blockIdx.x & 7), slot = (int)(blockIdx.x >> 3);
+  const int xlo = (int)((int64_t)xcd * ntiles / 8), xhi = (int)((int64_t)(xcd + 1) * ntiles / 8);
+  int T = xlo + slot;
+  if (T >= xhi) return;
+
+  // table-wide bound constants (meta row k)
+  const float* trow = p.c_meta + 4 * (int64_t)p.n_centers;
+  const float tscale = __uint_as_float(uni(__float_as_uint(trow[0])));
+  const float tgz = __uint_as_float(uni(__float_as_uint(trow[1])));
+  const float tgw = __uint_as_float(uni(__float_as_uint(trow[2])));
+  const float tgy = __uint_as_float(uni(__float_as_uint(trow[3])));
+  const int64_t lo_off = (int64_t)p.n_centers * kSDim;  // T3: the lo table follows the hi table
+  int* const dummy = p.work_count + 16;                 // sink of the fixed-count stores
+
+  // ---- header pipeline pieces -------------------------------------------------------------
+  // level 1: row indices (wave w: rows 32w..32w+31, lanes 0..31), candidate indices (wave w:
+  // candidates (w % (NT/2))*64 + lane; later waves repeat), residual centre rows (RL >= 1)
+  auto hdr_level1 = [&](const TileHdr& H, int par) {
+    const int lr = min(32 * wave + r, H.nrows - 1);
+    if (lane < 32)  // (exec-masked: still one vector-memory op of this wave)
+      dma4(p.row_index ? (const void*)(p.row_index + H.t0 + lr) : (const void*)p.seg_row_off,
+           uni(lds0 + L::kLand + wave * 128));
+    const int k = (wave % (NT / 2)) * 64 + lane;
+    const int kc = H.cnt > 0 ? min(k, H.cnt - 1) : 0;
+    dma4(p.cand_idx && H.cnt > 0 ? (const void*)(p.cand_idx + H.cbase + kc) : (const void*)p.seg_row_off,
+         uni(lds0 + L::kCidx + par * NT * 128 + (wave % (NT / 2)) * 256));
+    if (RL >= 1) {  // RL1: ca halves by wave parity; RL2: waves w%4 = 0,1 ca, 2,3 cb (the rest repeat)
+      const int half = wave & 1;
+      const bool second = RL == 2 && (wave & 2);
+      const float* src = second ? p.cb + (int64_t)H.cb_row * kSDim : p.ca + (int64_t)H.ca_row * kSDim;
+      dma16(src + half * 256 + lane * 4,
+            uni(lds0 + L::kRes + (par * RL + (second ? 1 : 0)) * kSDim * 4 + half * 1024));
+    }
+  };
+  // read level 1 (after the barrier that retires it): this wave's row ids and DMA sources of the tile
+  // DMA sources as 32-bit indices of 16-B units (row*128 + slot, candidate*64 + slot): the 64-bit
+  // address is one v_mad_u64_u32 per DMA, and a tile's sources cost 4 + NT/4 VGPRs, not twice that.
+  // Every DMA instruction moves whole 128-B row lines (8 lanes per row) or 64-B candidate pieces
+  // (4 lanes per candidate): fragment-shaped (16-B-per-row) DMAs double the address-path work.
+  struct Next {
+    uint32_t xi[4];
+    uint32_t ci[NT / 4];
+    int my_row;
+    float inv1;
+  };
+  auto cand_of = [&](const TileHdr& H, int par, int k) -> int {  // global centre of local candidate k
+    if (H.pen) return 0;
+    if (!p.cand_idx) return H.cbase + min(k, H.cnt - 1);
+    return reinterpret_cast<const int*>(smem + L::kCidx + par * NT * 128)[min(k, NT * 32 - 1)];
+  };
+  auto hdr_read1 = [&](const TileHdr& H, int par, Next& n) {
+    const int* land = reinterpret_cast<const int*>(smem + L::kLand + wave * 128);
+    auto row_of = [&](int lr) {  // lr: row within this wave's 32
+      return p.row_index ? land[lr] : H.t0 + min(32 * wave + lr, H.nrows - 1);
+    };
+    n.my_row = row_of(r);
+    // x image of wave w (4 KiB per stage): row rr at rr*128 B, 16-B slot q stored at q ^ ((rr>>1)&7)
+    // (conflict-free fragment reads); instruction i moves rows 8i + lane/8, physical slot lane%8
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int lr = 8 * i + (lane >> 3);
+      const int sl = (lane & 7) ^ ((lr >> 1) & 7);
+      n.xi[i] = (uint32_t)row_of(lr) * 128u + (uint32_t)sl;
+    }
+    // centre image: candidate k at k*64 B, slot q stored at q ^ ((k>>2)&3); instruction j of wave w
+    // moves candidates (w*NT/4 + j)*16 + lane/4, physical slot lane%4
+#pragma unroll
+    for (int j = 0; j < NT / 4; ++j) {
+      const int k = (wave * (NT / 4) + j) * 16 + (lane >> 2);
+      const int sl = (lane & 3) ^ ((k >> 2) & 3);
+      n.ci[j] = (uint32_t)cand_of(H, par, k) * 64u + (uint32_t)sl;
+    }
+  };
+  // level 2: |c|^2 and |c| of the candidates (SoA, gathered from meta), den_in of the rows (RL2 NORM)
+  auto hdr_level2 = [&](const TileHdr& H, int par, const Next& n) {
+    const int k = (wave % (NT / 2)) * 64 + lane;
+    const float* m = p.c_meta + 4 * (int64_t)cand_of(H, par, k);
+    dma4(m, uni(lds0 + L::kSoa + (par * 2 + 0) * NT * 128 + (wave % (NT / 2)) * 256));
+    dma4(m + 1, uni(lds0 + L::kSoa + (par * 2 + 1) * NT * 128 + (wave % (NT / 2)) * 256));
+    if (RL == 2 && lane < 32)
+      dma4(NORM ? (const void*)(p.den_in + n.my_row) : (const void*)p.seg_row_off, uni(lds0 + L::kLand + wave * 128));
+  };
+  auto hdr_read2 = [&](Next& n) {
+    if (RL == 2 && NORM) n.inv1 = 1.0f / reinterpret_cast<const float*>(smem + L::kLand + wave * 128)[r];
+    else n.inv1 = 1.0f;
+  };
+
+  // ---- ring ------------------------------------------------------------------------------------
+  const char* const xbase = reinterpret_cast<const char*>(p.x);
+  const char* const cbase16 = reinterpret_cast<const char*>(p.c16);
+  auto addr = [](const char* base, uint32_t unit) -> const void* {  // base + 16 unit (v_mad_u64_u32)
+    return base + (uint64_t)unit * 16u;
+  };
+  auto issue = [&](const Next& n, int c, int st) {
+    const uint32_t sb = lds0 + st * L::kStage;
+    const char* xb = xbase + c * (kSC * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma16_nt(addr(xb, n.xi[i]), uni(sb + wave * 4096 + i * 1024));
+    const char* cb = cbase16 + c * (kSC * 2);
+#pragma unroll
+    for (int j = 0; j < NT / 4; ++j) dma16(addr(cb, n.ci[j]), uni(sb + kSX + (wave * (NT / 4) + j) * 1024));
+    if (T3) {
+      const char* cl = cb + lo_off * 2;
+#pragma unroll
+      for (int j = 0; j < NT / 4; ++j)
+        dma16(addr(cl, n.ci[j]), uni(sb + kSX + L::kCen + (wave * (NT / 4) + j) * 1024));
+    }
+  };
+
+  // ---- first tile: synchronous header --------------------------------------------------------
+  TileHdr Hc = tile_header(p, tile_seg, seg_tile256, T);
+  Next cur{};
+  hdr_level1(Hc, 0);
+  wait_barrier<0>();
+  hdr_read1(Hc, 0, cur);
+  hdr_level2(Hc, 0, cur);
+  wait_barrier<0>();
+  hdr_read2(cur);
+#pragma unroll
+  for (int c = 0; c < kSS - 1; ++c) issue(cur, c, c);
+
+  const f32x16 zero16 = {};
+  bool first = true;
+  int par = 0;
+  int qb = 0;  // ring stage of this tile's chunk 0 (kNch % kSS != 0: the stage walks on across tiles)
+  for (;;) {
+    const int Tn = T + G8;
+    const bool more = Tn < xhi;
+    TileHdr Hn{};
+    Next nxt{};
+    // raw header words of the next tile (SMEM loads in flight; plain scalars so they stay in SGPRs)
+    int sN = 0, w_r0 = 0, w_r1 = 0, w_tb = 0, w_cnt = 0, w_cb = 0, w_fl = 0, w_ca = 0, w_cbr = 0;
+
+    f32x16 acc[NT];
+    f32x16 accl[T3 ? NT : 1];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = zero16;
+#pragma unroll
+    for (int t = 0; t < (T3 ? NT : 1); ++t) accl[t] = zero16;
+    double sv2 = 0.0;
+    f2 sf2v = {0.f, 0.f}, se2v = {0.f, 0.f}, se2l = {0.f, 0.f};
+    const float* lds_ca = reinterpret_cast<const float*>(smem + L::kRes + (par * RL + 0) * kSDim * 4);
+    const float* lds_cb = reinterpret_cast<const float*>(smem + L::kRes + (par * RL + (RL == 2 ? 1 : 0)) * kSDim * 4);
+    const float inv1 = cur.inv1;
+    const int xsw = (r >> 1) & 7;  // x image swizzle of this lane's row
+    const int csw = (r >> 2) & 3;  // centre image swizzle of this lane's candidate rows
+
+#pragma unroll 1
+    for (int c = 0; c < kNch; ++c) {
+      // wait for chunk c: the younger ops are chunk c+1 and the groups issued after chunk c.  After
+      // the first tile, chunk 2 was issued at the start of the previous epilogue, before its E
+      // stores: c = 0 sees chunks 1, 2 + E, c = 1, 2 see one chunk + E.  Header level 1 (issued at
+      // c = 2) is younger than chunks 3, 4, level 2 (c = 5) than chunks 6, 7.  The barrier then also
+      // frees stage (c-1) % kSS.
+      if (more || c + 1 < kNch) {
+        if (!first && c == 0) wait_barrier<2 * P + L::E>();
+        else if (!first && c <= 2) wait_barrier<P + L::E>();
+        else if (c >= 3 && c <= 4 && more) wait_barrier<P + L::H1>();
+        else if (c >= 6 && c <= 7 && more) wait_barrier<P + L::H2>();
+        else wait_barrier<P>();
+      } else {
+        wait_barrier<0>();
+      }
+      const int st = (qb + c) % kSS;
+      if (c + kSS - 1 < kNch) {
+        if (first || c != 0) issue(cur, c + kSS - 1, (qb + c + kSS - 1) % kSS);
+      } else if (more) {
+        issue(nxt, c + kSS - 1 - kNch, (qb + c + kSS - 1) % kSS);
+      }
+      if (more) {
+        if (c == 0) sN = sload(tile_seg + Tn);
+        if (c == 1) {  // this iteration's wait_barrier retired the tile_seg load (lgkmcnt(0))
+          SGPR_PIN(sN);
+          w_r0 = sload(p.seg_row_off + sN);
+          w_r1 = sload(p.seg_row_off + sN + 1);
+          w_tb = sload(seg_tile256 + sN);
+          w_cnt = sload(p.cand_count + sN);
+          w_cb = sload(p.cand_base + sN);
+          if (p.seg_flags)  // the aligned dword holding byte sN
+            w_fl = sload(reinterpret_cast<const void*>(reinterpret_cast<uintptr_t>(p.seg_flags + sN) & ~(uintptr_t)3));
+          if (p.seg_ca) w_ca = sload(p.seg_ca + sN);
+          if (p.seg_cb) w_cbr = sload(p.seg_cb + sN);
+        }
+        if (c == 2) {  // ... and this one the segment words
+          SGPR_PIN(w_r0); SGPR_PIN(w_r1); SGPR_PIN(w_tb); SGPR_PIN(w_cnt);
+          SGPR_PIN(w_cb); SGPR_PIN(w_fl); SGPR_PIN(w_ca); SGPR_PIN(w_cbr);
+          Hn.T = Tn;
+          Hn.s = sN;
+          Hn.t0 = w_r0 + (Tn - w_tb) * kSR;
+          Hn.nrows = min(kSR, w_r1 - Hn.t0);
+          Hn.cnt = w_cnt;
+          Hn.cbase = w_cb;
+          Hn.flag = p.seg_flags && ((w_fl >> (8 * (sN & 3))) & RQSID_SEG_PENALTY);
+          Hn.pen = Hn.flag || Hn.cnt <= 0;
+          Hn.ca_row = p.seg_ca ? w_ca : sN;
+          Hn.cb_row = p.seg_cb ? w_cbr : sN;
+          hdr_level1(Hn, par ^ 1);
+        }
+        if (c == 5) {
+          hdr_read1(Hn, par ^ 1, nxt);
+          hdr_level2(Hn, par ^ 1, nxt);
+        }
+        if (c == 8) hdr_read2(nxt);
+      }
+#if RQSID_AB_MODE < 3
+      // compute chunk c (dims 32c .. 32c+31) in two k-steps: lane (r, h) owns row r of its wave and
+      // dims 32c + 16ks + 8h + 0..7 (the per-tile kernel's fragment layout)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+      const unsigned char* xb = smem + st * L::kStage + (32 * wave + r) * 128;
+      const int q0 = 4 * ks + 2 * h;
+      const float4 xa = *reinterpret_cast<const float4*>(xb + ((q0 ^ xsw) << 4));
+      const float4 xc = *reinterpret_cast<const float4*>(xb + (((q0 + 1) ^ xsw) << 4));
+      f2 v[4] = {f2{xa.x, xa.y}, f2{xa.z, xa.w}, f2{xc.x, xc.y}, f2{xc.z, xc.w}};
+      const int d0 = c * kSC + 16 * ks + 8 * h;
+      if (RL >= 1) {
+        const float4 a0 = *reinterpret_cast<const float4*>(lds_ca + d0);
+        const float4 a1 = *reinterpret_cast<const float4*>(lds_ca + d0 + 4);
+        const f2 av[4] = {f2{a0.x, a0.y}, f2{a0.z, a0.w}, f2{a1.x, a1.y}, f2{a1.z, a1.w}};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] - av[e];  // exact fp32, as the reference
+      }
+      if (RL >= 2) {
+        const float4 b0 = *reinterpret_cast<const float4*>(lds_cb + d0);
+        const float4 b1 = *reinterpret_cast<const float4*>(lds_cb + d0 + 4);
+        const f2 bv[4] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1.x, b1.y}, f2{b1.z, b1.w}};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (NORM ? v[e] * inv1 : v[e]) - bv[e];
+      }
+      h2 hh[4], lh[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) hh[e] = __builtin_convertvector(v[e], h2);
+      const f16x8 bf = __builtin_shufflevector(__builtin_shufflevector(hh[0], hh[1], 0, 1, 2, 3),
+                                               __builtin_shufflevector(hh[2], hh[3], 0, 1, 2, 3), 0, 1, 2, 3, 4, 5,
+                                               6, 7);
+      if (T3) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const f2 xs = (v[e] - __builtin_convertvector(hh[e], f2)) * 4096.0f;  // exact
+          lh[e] = __builtin_convertvector(xs, h2);
+          const f2 ev = xs - __builtin_convertvector(lh[e], f2);  // exact
+          se2l = ev * ev + se2l;
+        }
+      }
+      f16x8 bl = {};
+      if (T3)
+        bl = __builtin_shufflevector(__builtin_shufflevector(lh[0], lh[1], 0, 1, 2, 3),
+                                     __builtin_shufflevector(lh[2], lh[3], 0, 1, 2, 3), 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const f2 ex = v[e] - __builtin_convertvector(hh[e], f2);  // exact: the fp16 rounding residual
+        se2v = ex * ex + se2v;
+        if (NORM && RL >= 1) {
+          sv2 = fma((double)v[e].x, (double)v[e].x, sv2);
+          sv2 = fma((double)v[e].y, (double)v[e].y, sv2);
+        } else {
+          sf2v = v[e] * v[e] + sf2v;
+        }
+      }
+      const unsigned char* cimg = smem + st * L::kStage + kSX + r * 64 + (((2 * ks + h) ^ csw) << 4);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const f16x8 af = *reinterpret_cast<const f16x8*>(cimg + t * 32 * 64);
+#if RQSID_AB_MODE >= 2
+        acc[t][0] += (float)bf[0] + (float)af[0];
+#else
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[t], 0, 0, 0);
+        if (T3) {
+          const f16x8 al = *reinterpret_cast<const f16x8*>(cimg + L::kCen + t * 32 * 64);
+          accl[T3 ? t : 0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bl, accl[T3 ? t : 0], 0, 0, 0);
+          accl[T3 ? t : 0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bf, accl[T3 ? t : 0], 0, 0, 0);
+        }
+#endif
+      }
+      }  // ks
+#endif
+    }
+
+    // the next tile's chunk 2 goes into chunk 15's stage as soon as every wave is done with it, so
+    // three chunks stream during the epilogue (VALU only) instead of two
+    if (more) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      issue(nxt, kSS - 1, (qb + kNch - 1) % kSS);
+    }
+    // ---- epilogue (tile T): the single-pass bound of assign_screen_kernel<..., ONE> ----------
+    const bool row_valid = 32 * wave + r < Hc.nrows;
+    const int my_row = cur.my_row;
+    float inv_den = 1.f, dr = 0.f, vn, en, en2 = 0.f;
+    {
+      const float se2 = se2v.x + se2v.y, sf2 = sf2v.x + sf2v.y;
+      en = sqrtf(se2 + __shfl_xor(se2, 32)) * 1.001f + 1e-30f;
+      if (T3) {
+        const float l2 = se2l.x + se2l.y;
+        en2 = sqrtf(l2 + __shfl_xor(l2, 32)) * (1.001f / 4096.0f) + 1e-30f;
+      }
+      float nrm;
+      if (NORM && RL >= 1) {
+        const double tot = sv2 + __shfl_xor(sv2, 32);
+        nrm = (float)sqrt(tot);
+        const float den = nrm + 1e-8f;
+        inv_den = 1.0f / den;
+        if (RL == 1) {  // fixed-count store (dummy target for the other half / padding rows)
+          float* dst = (h == 0 && row_valid) ? p.den_out + my_row : reinterpret_cast<float*>(dummy);
+          *dst = den;
+        }
+        dr = RL == 1 ? 2.0f * 5.97e-8f : (4.0f * 2.39e-7f * (1.0f + nrm) * inv_den + 4.0f * 5.97e-8f);
+      } else {
+        nrm = sqrtf(sf2 + __shfl_xor(sf2, 32));
+      }
+      vn = nrm * 1.0001f + 1e-30f;
+    }
+    int out_l = kSentinel, out_g = kSentinel;
+    bool need = false;
+    WorkItem w{};
+    w.row = my_row;
+    w.seg = Hc.s;
+    if (Hc.pen) {
+      need = true;
+      w.n = Hc.flag ? -2 : -3;
+    } else {
+#if RQSID_AB_MODE >= 1
+      float sink = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) sink += acc[t][v] + (T3 ? accl[T3 ? t : 0][v] : 0.f);
+      const int k = sink == -1.2345e38f ? 1 : (int)(((uint32_t)my_row * 2654435761u) >> 8) % Hc.cnt;
+      out_l = p.cand_lid ? 0 : k;
+      out_g = cand_of(Hc, par, k);
+#else
+      const float hn = vn + en;
+      const float vr = vn * inv_den;
+      const float ar = p.acc_rel, ar2 = 2.0f * p.acc_rel, k2 = 2.0f * inv_den * 1.000001f;
+      const float A = T3 ? k2 * (en2 + ar * hn + ar2 * (en + en2)) + 2.0f * dr + 7.2e-7f * vr
+                         : k2 * (en + ar * hn) + 2.0f * dr + 4.8e-7f * vr;
+      const float B = T3 ? k2 * (hn * (1.0f + ar2) + 2.0f * (en + en2)) : k2 * hn * (1.0f + ar);
+      const float C = T3 ? k2 * ((en + en2) + ar * hn + ar2 * (hn + en + en2)) : 0.0f;
+      const float m2 = -2.0f * inv_den * tscale;
+      const float A2 = (A + B * (T3 ? tgz : tgw) + C * tgw + 2.39e-7f * tgy) * 1.000001f;
+      const f2 m2v = {m2, m2}, a2v = {A2, A2}, epsv = {1e-30f, 1e-30f};
+      const float* m_csq = reinterpret_cast<const float*>(smem + L::kSoa + (par * 2 + 0) * NT * 128);
+      const float* m_y = reinterpret_cast<const float*>(smem + L::kSoa + (par * 2 + 1) * NT * 128);
+      float U = INFINITY;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 csq = *reinterpret_cast<const float4*>(m_csq + t * 32 + 8 * g + 4 * h);
+          const float4 yy = *reinterpret_cast<const float4*>(m_y + t * 32 + 8 * g + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int v = 4 * g + 2 * e;
+            f2 d = {acc[t][v], acc[t][v + 1]};
+            if (T3) d = f2{accl[T3 ? t : 0][v], accl[T3 ? t : 0][v + 1]} * 0x1p-12f + d;
+            const f2 P2 = m2v * d + (e ? f2{csq.z, csq.w} : f2{csq.x, csq.y});
+            const f2 E2 = a2v * (e ? f2{yy.z, yy.w} : f2{yy.x, yy.y}) + epsv;
+            const f2 ub = P2 + E2, lb = P2 - E2;
+            U = fminf(U, fminf(ub.x, ub.y));
+            acc[t][v] = lb.x;
+            acc[t][v + 1] = lb.y;
+          }
+        }
+      }
+      U = fminf(U, __shfl_xor(U, 32));
+      const float Up = fmaf(fabsf(U), 0x1p-22f, U) + 1.2e-38f;
+      const f2 upv = {Up, Up};
+      uint32_t pbits[NT / 2];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t b = (t & 1) ? pbits[t >> 1] : 0u;
+#pragma unroll
+        for (int v = 0; v < 16; v += 2) {
+          const f2 d = f2{acc[t][v], acc[t][v + 1]} - upv;
+          b = __builtin_amdgcn_alignbit(b, __float_as_uint(d.x), 31);
+          b = __builtin_amdgcn_alignbit(b, __float_as_uint(d.y), 31);
+        }
+        pbits[t >> 1] = b;
+      }
+      // candidates beyond cnt (duplicates of the last one) never pass
+      // (a lane half's candidates ascend with v, so a tile's valid values are a prefix of its 16 bits)
+      if (Hc.cnt < NT * 32) {
+#pragma unroll
+        for (int wd = 0; wd < NT / 2; ++wd) {
+          uint32_t m = 0;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int rem = Hc.cnt - 32 * (2 * wd + q) - 4 * h;  // valid iff (v&3) + 8(v>>2) < rem
+            int nv = 0;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) nv += min(4, max(0, rem - 8 * g));
+            const uint32_t pre = (uint32_t)((0xFFFFull << (16 - nv)) & 0xFFFFull);
+            m |= q == 0 ? pre << 16 : pre;
+          }
+          pbits[wd] &= m;
+        }
+      }
+      int k = -1;
+      if (pass_decide(pbits, h, k, w)) {
+        out_l = k;
+        out_g = cand_of(Hc, par, k);
+      } else {
+        need = true;
+      }
+#endif
+    }
+    {  // fixed-count output stores: exactly E per wave whatever the rows decided
+      const bool mine = h == 0 && row_valid;
+      int* dl = mine ? p.out_local + my_row : dummy;
+      int* dg = mine ? p.out_global + my_row : dummy;
+      *dl = out_l;
+      *dg = out_g;
+    }
+    if (need && h == 0 && row_valid) p.work[my_row] = w;  // may only strengthen the next counted waits
+
+    if (!more) break;
+    T = Tn;
+    Hc = Hn;
+    cur = nxt;
+    par ^= 1;
+    qb = (qb + kNch) % kSS;
+    first = false;
+  }
+}
+
+// 256-row tiling of the segments: seg_tile256[s] = sum_{s' < s} ceil(rows(s') / 256) (one block)
+__global__ __launch_bounds__(1024) void stream_tiles_kernel(const int32_t* __restrict__ seg_row_off, int nseg,
+                                                            int32_t* __restrict__ seg_tile256) {
+  __shared__ int part[1024];
+  const int tid = threadIdx.x;
+  const int per = (nseg + 1023) / 1024, s0 = min(nseg, tid * per), s1 = min(nseg, s0 + per);
+  int sum = 0;
+  for (int s = s0; s < s1; ++s) sum += (seg_row_off[s + 1] - seg_row_off[s] + kSR - 1) / kSR;
+  part[tid] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+    const int v = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int run = part[tid] - sum;
+  for (int s = s0; s < s1; ++s) {
+    seg_tile256[s] = run;
+    run += (seg_row_off[s + 1] - seg_row_off[s] + kSR - 1) / kSR;
+  }
+  if (tid == 1023) seg_tile256[nseg] = part[1023];
+}
+
+// tile -> segment map (one thread per tile, binary search over seg_tile256)
+__global__ __launch_bounds__(256) void tile_seg_kernel(const int32_t* __restrict__ seg_tile256, int nseg,
+                                                       int64_t cap, int32_t* __restrict__ tile_seg) {
+  const int ntiles = seg_tile256[nseg];
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < ntiles && t < cap; t += (int64_t)gridDim.x * 256) {
+    int lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (seg_tile256[mid] <= t) lo = mid; else hi = mid;
+    }
+    tile_seg[t] = lo;
+  }
+}
+
+template <int NT, int RL, bool NORM, bool T3>
+bool launch_one(const AssignParams& p, const int32_t* tile_seg, const int32_t* seg_tile256, int64_t max_tiles,
+                hipStream_t st) {
+  using L = StreamLayout<NT, RL, NORM, T3>;
+  static int ncu = 0;
+  static bool attr = false;
+  if (!ncu) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+    ncu = prop.multiProcessorCount;
+  }
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)assign_stream_kernel<NT, RL, NORM, T3>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, L::kBytes) != hipSuccess)
+      return false;
+    attr = true;
+  }
+  int64_t g = ncu;  // one 8-wave block per CU
+  if (g > max_tiles) g = max_tiles;
+  g = g / 8 * 8;
+  if (g < 8) g = 8;
+  hipLaunchKernelGGL((assign_stream_kernel<NT, RL, NORM, T3>), dim3((unsigned)g), dim3(kSW * 64), L::kBytes, st, p,
+                     tile_seg, seg_tile256);
+  return true;
+}
+
+}  // namespace
+
+bool stream_supported(int nt, bool t3, int rl, bool norm) {
+  (void)norm;
+  if (nt == 8) return !t3 && rl >= 0 && rl <= 2;
+  if (nt == 4) return rl >= 0 && rl <= 2;
+  return false;
+}
+
+void launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
+                          int32_t* seg_tile256, int64_t cap, hipStream_t st) {
+  hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, seg_tile256);
+  const int64_t max_tiles = cap / kSR + p.n_segments;  // bound on the 256-row tiles
+  const unsigned tg = (unsigned)(max_tiles / 256 + 1 < 4096 ? max_tiles / 256 + 1 : 4096);
+  hipLaunchKernelGGL(tile_seg_kernel, dim3(tg), dim3(256), 0, st, seg_tile256, p.n_segments, cap, tile_seg);
+#define RQ_L(NT, RL, NORM, T3) launch_one<NT, RL, NORM, T3>(p, tile_seg, seg_tile256, max_tiles, st)
+  if (nt == 8) {
+    if (rl == 0) RQ_L(8, 0, false, false);
+    else if (rl == 1) { if (norm) RQ_L(8, 1, true, false); else RQ_L(8, 1, false, false); }
+    else { if (norm) RQ_L(8, 2, true, false); else RQ_L(8, 2, false, false); }
+  } else if (t3) {
+    if (rl == 0) RQ_L(4, 0, false, true);
+    else if (rl == 1) { if (norm) RQ_L(4, 1, true, true); else RQ_L(4, 1, false, true); }
+    else { if (norm) RQ_L(4, 2, true, true); else RQ_L(4, 2, false, true); }
+  } else {
+    if (rl == 0) RQ_L(4, 0, false, false);
+    else if (rl == 1) { if (norm) RQ_L(4, 1, true, false); else RQ_L(4, 1, false, false); }
+    else { if (norm) RQ_L(4, 2, true, false); else RQ_L(4, 2, false, false); }
+  }
+#undef RQ_L
+}
+
+}  // namespace rqsid

@@ -43,7 +43,8 @@ const char* rqsid_last_error(void);
  * scaled values outside the fp16 normal range stored as 0 (the MFMA must never see a subnormal).
  * c16 [2][k][dim] (IEEE half bits: the hi table, then the lo table); c_meta [k+1][4]: row j <  k =
  * {|c|^2, |c|, |c - (hi + lo 2^-12) 2^-s|, |c - hi 2^-s|} (fp64-accumulated, feeding the screening
- * error bound), row k = {2^-s, 0, 0, 0}.  Replaces the per-call centre side of torch.cdist's
+ * error bound), row k = {2^-s, max_j |c - (hi + lo 2^-12) 2^-s| / |c|, max_j |c - hi 2^-s| / |c|,
+ * max_j |c|} (rounded up; the single-pass screens collapse their per-candidate bound onto |c|).  Replaces the per-call centre side of torch.cdist's
  * mm-expansion (ATen _euclidean_dist) used by pairwise_distance_full,
  * balancekmeans/__init__.py:576-603. */
 int rqsid_prepare_centers(const float* centers, int64_t k, int32_t dim,

@@ -330,3 +330,59 @@ def test_multigroup_weighted_encode_vs_oracle():
     ref = O.encode(x, [cb["c0"], cb["c1"], cb["c2"]], [16, 16, 32], cb["match"], gd, w, residual_from_weighted=True,
                    exact=True)
     assert (got == ref).all()
+
+
+def _with_variant(v, fn):
+    import os
+    old = os.environ.get("RQSID_SCREEN_VARIANT")
+    os.environ["RQSID_SCREEN_VARIANT"] = str(v)
+    try:
+        return fn()
+    finally:
+        if old is None:
+            del os.environ["RQSID_SCREEN_VARIANT"]
+        else:
+            os.environ["RQSID_SCREEN_VARIANT"] = old
+
+
+@pytest.mark.parametrize("shape", ["small", "prod"])
+@pytest.mark.parametrize("sem_name", ["train", "simplified"])
+def test_stream_kernel_equals_tile_kernel(shape, sem_name):
+    """The persistent streamed screen (assign_stream.hip, RQSID_SCREEN_VARIANT=5) and the per-tile
+    screen (assign.hip) return the exact argmin both: identical IDs on every level, with
+    partial candidate lists (32 of a 128-wide tile), penalty-free match lists and both semantics;
+    the streamed run is also checked row by row against the fp64 oracle on a sample."""
+    sem = {"train": HIERARCHICAL_TRAIN, "simplified": SIMPLIFIED}[sem_name]
+    if shape == "small":
+        need, cb = (16, 16, 32), synth.encode_codebooks(seed=5, need=(16, 16, 32), n_cand=320, pool_rows=8192)
+    else:
+        need, cb = (128, 128, 256), synth.encode_codebooks(seed=99)
+    xn = synth.mixture_rows(0, 40000)
+    x = gpu(xn)
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], list(need),
+                    match=torch.from_numpy(cb["match"]), semantics=sem, device=DEV)
+    a = _with_variant(5, lambda: enc.encode(x).cpu().numpy())
+    b = _with_variant(0, lambda: enc.encode(x).cpu().numpy())
+    assert (a == b).all(), f"{int((a != b).any(1).sum())} rows differ between the streamed and per-tile screens"
+    sel = np.arange(0, 40000, 37)
+    ref = O.encode(xn[sel], [cb["c0"], cb["c1"], cb["c2"]], list(need), cb["match"],
+                   normalize=sem.normalize_residual, remap_last=sem.remap_last,
+                   last_group_mult=sem.last_group_mult, residual_from_weighted=True, exact=True) \
+        if sem_name == "simplified" else \
+        O.encode(xn[sel], [cb["c0"], cb["c1"], cb["c2"]], list(need), cb["match"], residual_from_weighted=True,
+                 exact=True)
+    assert (a[sel] == ref).all()
+
+
+@pytest.mark.parametrize("k", [100, 128, 200, 256])
+def test_stream_nearest_partial_tiles(k):
+    """Single-segment nearest with k < NT*32 candidates (padding lanes masked) on the streamed path."""
+    rng = np.random.default_rng(k)
+    c = rng.standard_normal((k, 512)).astype(np.float32)
+    x = (c[rng.integers(0, k, 30000)] + 0.3 * rng.standard_normal((30000, 512))).astype(np.float32)
+    pc = ops.prepare_centers(gpu(c))
+    got = _with_variant(5, lambda: ops.nearest(gpu(x), pc).cpu().numpy())
+    tile = _with_variant(0, lambda: ops.nearest(gpu(x), pc).cpu().numpy())
+    assert (got == tile).all()
+    sel = np.arange(0, 30000, 29)
+    assert (got[sel] == exact_ids(x[sel], c)).all()
