@@ -149,12 +149,17 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
   const int b = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   const int nseg = p.n_segments;
   if (b >= p.seg_tile_off[nseg]) return;
-  int lo = 0, hi = nseg;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (p.seg_tile_off[mid] <= b) lo = mid; else hi = mid;
+  int s;
+  if (p.tile_seg) {  // one load instead of log2(S) dependent ones (14 at the last level)
+    s = p.tile_seg[b];
+  } else {
+    int lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (p.seg_tile_off[mid] <= b) lo = mid; else hi = mid;
+    }
+    s = lo;
   }
-  const int s = lo;
   const int t0 = p.seg_row_off[s] + (b - p.seg_tile_off[s]) * kTileRows;
   const int nrows = min(kTileRows, p.seg_row_off[s + 1] - t0);
   const int cnt = p.cand_count[s];
@@ -764,6 +769,20 @@ __global__ __launch_bounds__(256) void assign_rescore_kernel(AssignParams p) {
   }
 }
 
+// tile -> segment map of the per-tile screen (one thread per tile, binary search of seg_tile_off)
+__global__ __launch_bounds__(256) void tile_seg128_kernel(const int32_t* __restrict__ seg_tile_off, int nseg,
+                                                          int64_t cap, int32_t* __restrict__ tile_seg) {
+  const int ntiles = seg_tile_off[nseg];
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < ntiles && t < cap; t += (int64_t)gridDim.x * 256) {
+    int lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (seg_tile_off[mid] <= t) lo = mid; else hi = mid;
+    }
+    tile_seg[t] = lo;
+  }
+}
+
 // Stream-path compaction: rows whose out_global is the re-score sentinel (-2) -> work_idx list.
 // One atomic per block: the block counts the sentinels of its 16K-row range, reserves, then lists
 // (the row order inside the list is irrelevant).  A per-wave atomic serialises on the one counter.
@@ -1002,6 +1021,14 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
     hipLaunchKernelGGL(sentinel_compact_kernel, dim3((unsigned)cdiv(n_rows, kCompactRows)), dim3(256), 0, st, out_global,
                        n_rows, p.work_count, work_idx);
     p.work_idx = work_idx;
+  } else {
+    if (n_segments > 1) {  // (tiles <= rows: the map fits its workspace slot)
+      hipLaunchKernelGGL(tile_seg128_kernel, dim3(grid_cap(cdiv(max_tiles, 256), 4096)), dim3(256), 0, st, seg_tile_off,
+                         n_segments, n_rows, tile_seg);
+      p.tile_seg = tile_seg;
+    }
+  }
+  if (use_stream) {
   } else if (t3) launch_screen2<4, 2, true>(p, res_levels, norm, grid, !legacy, st);
   else if (cand_count_max <= 128) launch_screen2<4, 2, false>(p, res_levels, norm, grid, !legacy, st);
   else if (cand_count_max <= 256) launch_screen2<8, 2, false>(p, res_levels, norm, grid, !legacy, st);

@@ -57,6 +57,7 @@ struct AssignParams {
   WorkItem* work;
   int32_t* work_count;
   const int32_t* work_idx;  // NULL: work[] is the compact list; else the list is work[work_idx[i]]
+  const int32_t* tile_seg;  // tile -> segment (per-tile screen; NULL: binary search of seg_tile_off)
   int64_t work_cap;
   float acc_rel;
   int32_t terms;          // 1 or 3 (screen product terms; host-side dispatch only)
