@@ -20,7 +20,7 @@ SRCS = [PKG / "csrc" / "rqsid.hip", PKG / "csrc" / "assign.hip", PKG / "csrc" / 
 DEPS = SRCS + [PKG / "csrc" / "internal.h", PKG / "csrc" / "assign_common.h"]
 HEADER = REPO / "include" / "rqsid.h"
 
-HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC"]
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-shared", "-fPIC"]
 
 c_i32, c_i64, c_f32, c_vp, c_char_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_char_p
 

@@ -94,6 +94,10 @@ __global__ void centers_scale_kernel(float* __restrict__ scale) {
 // ---------------------------------------------------------------------------
 // screening kernel
 // ---------------------------------------------------------------------------
+#ifndef RQSID_INTERLEAVE  // 1: the ring's DMA ops interleaved with the MFMAs of the compute phase
+#define RQSID_INTERLEAVE 0
+#endif
+
 template <int NT, int S, bool T3>
 struct ScreenLayout {
   static constexpr int kCHalf = NT * 32 * 64;              // NT*32 candidates x 32 fp16 dims
@@ -130,6 +134,10 @@ struct ScreenLayout {
 // and every candidate costs two packed FMAs for P = |c|^2 - 2 v.c/den and E, two packed adds for
 // ub = P + E / lb = P - E (lb overwrites the accumulator) and half a min3 (sweep 1), then a compare
 // and two selects (sweep 2: how many candidates have lb <= U, the last two of them).
+#ifdef RQSID_STAMPS
+__device__ unsigned long long g_stamps_tile[4];
+#endif
+
 template <int NT, int S, int RL, bool NORM, bool T3, bool ONE>
 __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <= 3) ? 2 : 1))) void assign_screen_kernel(AssignParams p) {
   using L = ScreenLayout<NT, S, T3>;
@@ -143,6 +151,7 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, r = lane & 31;
+  ST(const uint64_t st_begin = ST_NOW(); uint64_t st_wait = 0; uint64_t st_e0 = 0; uint64_t st_issue = 0;)
   // XCD-aware tile order: blocks b and b+8 share an XCD (and its L2), so give each group of 8 a
   // contiguous run of tiles -> a segment's candidate centres stay hot in one L2 (gridDim.x % 8 == 0)
   const int G = gridDim.x;
@@ -217,9 +226,7 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
     lk[j] = -1;
     llb[j] = INFINITY;
   }
-  double sv2 = 0.0;            // sum v^2 in fp64 (NORM: the normalising denominator is exact)
-  f2 sf2v = {0.f, 0.f}, se2v = {0.f, 0.f};  // sum v^2 (fp32, bound only), sum (v - fp16(v))^2
-  f2 se2l = {0.f, 0.f};                      // T3: sum of the second term's residual^2 (units 2^-12)
+  RowSums rs;  // the bound's running sums (row_frag)
   float vn = 0.f, en = 0.f, en2 = 0.f, inv_den = 1.f, dr = 0.f;
   float4* lds_meta = reinterpret_cast<float4*>(smem + L::kMeta);
   const f32x16 zero16 = {};
@@ -242,7 +249,11 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
       const int kl = pbase + il < cnt ? pbase + il : cnt - 1;
       const int cg = cand_global(p, cbase, kl);
       const int slot = (lane & 3) ^ ((il >> 2) & 3);
+#ifdef RQSID_AB_CMAJOR  // timing probe: chunk-major centre layout [dim/32][k][32] (wrong data)
+      csrc[j] = reinterpret_cast<const _Float16*>(p.c16) + (int64_t)cg * kChunk + slot * 8;
+#else
       csrc[j] = reinterpret_cast<const _Float16*>(p.c16) + (int64_t)cg * dim + slot * 8;
+#endif
       if (T3) clo[j] = csrc[j] + (int64_t)p.n_centers * dim;
     }
     __syncthreads();
@@ -287,25 +298,39 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
 #pragma unroll
     for (int t = 0; t < (T3 ? NT : 1); ++t) accl[t] = zero16;
 
-    auto issue = [&](int c) {
+#ifdef RQSID_AB_CMAJOR
+    const int64_t kCStride = (int64_t)p.n_centers * kChunk;
+#else
+    constexpr int kCStride = kChunk;
+#endif
+    // DMA op i of chunk c (x rows 0..3, hi centres, lo centres) into stage c % S
+    auto issue_op = [&](int c, int i, bool relaxed) {
       const uint32_t sb = lds0 + (uint32_t)((c % S) * L::kStage);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        dma16_nt(xsrc[i] + c * kChunk, __builtin_amdgcn_readfirstlane(sb + wave * kXWaveBytes + i * 1024));
-#pragma unroll
-      for (int j = 0; j < NT / 2; ++j)
-        dma16(csrc[j] + c * kChunk, __builtin_amdgcn_readfirstlane(sb + kXStage + (wave * (NT / 2) + j) * 1024));
-      if (T3) {
-#pragma unroll
-        for (int j = 0; j < NT / 2; ++j)
-          dma16(clo[j] + c * kChunk,
-                __builtin_amdgcn_readfirstlane(sb + kXStage + L::kCHalf + (wave * (NT / 2) + j) * 1024));
+      if (i < 4) {
+        const void* src = xsrc[i] + c * kChunk;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(sb + wave * kXWaveBytes + i * 1024);
+        if (relaxed) dma16_nt_r(src, dst); else dma16_nt(src, dst);
+      } else {
+        const int j = (i - 4) % (NT / 2), lo = (i - 4) / (NT / 2);
+        const void* src = (lo ? clo[T3 ? j : 0] : csrc[j]) + c * kCStride;
+        const uint32_t dst =
+            __builtin_amdgcn_readfirstlane(sb + kXStage + lo * L::kCHalf + (wave * (NT / 2) + j) * 1024);
+        if (relaxed) dma16_r(src, dst); else dma16(src, dst);
       }
     };
-    auto compute = [&](int c) {
+    auto issue = [&](int c) {
+#pragma unroll
+      for (int i = 0; i < P; ++i) issue_op(c, i, false);
+    };
+    // compute chunk c; the P DMA ops of chunk cn (< 0: none) are spread between its 2*NT MFMA groups,
+    // so a DMA issue stall (the load path's back-pressure) overlaps MFMAs in flight instead of
+    // preceding the whole phase
+    auto compute = [&](int c, int cn) {
 #if RQSID_AB_MODE >= 3
+      if (cn >= 0) issue(cn);
       return;
 #endif
+      constexpr int NG = 2 * NT;
       const unsigned char* xb = smem + (c % S) * L::kStage + wave * kXWaveBytes + r * 128;
       const unsigned char* cbp = smem + (c % S) * L::kStage + kXStage + r * 64;
 #pragma unroll
@@ -313,60 +338,10 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
         const int q0 = 4 * ks + 2 * h;
         const float4 xa = *reinterpret_cast<const float4*>(xb + ((q0 ^ xsw) << 4));
         const float4 xc = *reinterpret_cast<const float4*>(xb + (((q0 + 1) ^ xsw) << 4));
-        // packed fp32 pairs: every VALU op below handles two elements (v_pk_*), the fp16 conversion
-        // is v_cvt_pk_f16_f32 (round to nearest even).  fp16 inputs keep denormals (hipcc's default
-        // MODE; pinned by tests/test_mfma_numerics.py::test_f16_denormals_are_kept) and an input
-        // beyond the fp16 range becomes inf, which makes the row's bound infinite -> exact re-score.
-        f2 v[4] = {f2{xa.x, xa.y}, f2{xa.z, xa.w}, f2{xc.x, xc.y}, f2{xc.z, xc.w}};
         const int d0 = c * kChunk + 16 * ks + 8 * h;
-        if (RL >= 1) {
-          const float4 a0 = *reinterpret_cast<const float4*>(lds_ca + d0);
-          const float4 a1 = *reinterpret_cast<const float4*>(lds_ca + d0 + 4);
-          const f2 av[4] = {f2{a0.x, a0.y}, f2{a0.z, a0.w}, f2{a1.x, a1.y}, f2{a1.z, a1.w}};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = v[e] - av[e];  // exact fp32, as the reference
-        }
-        if (RL >= 2) {
-          const float4 b0 = *reinterpret_cast<const float4*>(lds_cb + d0);
-          const float4 b1v = *reinterpret_cast<const float4*>(lds_cb + d0 + 4);
-          const f2 bv[4] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1v.x, b1v.y}, f2{b1v.z, b1v.w}};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (NORM ? v[e] * inv1 : v[e]) - bv[e];
-        }
-        h2 hh[4], lh[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) hh[e] = __builtin_convertvector(v[e], h2);
-        const f16x8 bf = __builtin_shufflevector(__builtin_shufflevector(hh[0], hh[1], 0, 1, 2, 3),
-                                                 __builtin_shufflevector(hh[2], hh[3], 0, 1, 2, 3),
-                                                 0, 1, 2, 3, 4, 5, 6, 7);
-        if (T3) {  // second term: the fp16 rounding residual scaled by 2^12 (fp16 normal range)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const f2 xs = (v[e] - __builtin_convertvector(hh[e], f2)) * 4096.0f;  // exact
-            lh[e] = __builtin_convertvector(xs, h2);
-            if (pass == 0) {
-              const f2 ev = xs - __builtin_convertvector(lh[e], f2);  // exact
-              se2l = ev * ev + se2l;
-            }
-          }
-        }
-        f16x8 bl = {};
-        if (T3)
-          bl = __builtin_shufflevector(__builtin_shufflevector(lh[0], lh[1], 0, 1, 2, 3),
-                                       __builtin_shufflevector(lh[2], lh[3], 0, 1, 2, 3), 0, 1, 2, 3, 4, 5, 6, 7);
-        if (pass == 0) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const f2 ex = v[e] - __builtin_convertvector(hh[e], f2);  // exact: the fp16 rounding residual
-            se2v = ex * ex + se2v;
-            if (NORM && RL >= 1) {
-              sv2 = fma((double)v[e].x, (double)v[e].x, sv2);
-              sv2 = fma((double)v[e].y, (double)v[e].y, sv2);
-            } else {
-              sf2v = v[e] * v[e] + sf2v;
-            }
-          }
-        }
+        f16x8 bf, bl = {};
+        if (pass == 0) row_frag<RL, NORM, T3, true>(xa, xc, lds_ca, lds_cb, d0, inv1, bf, bl, rs);
+        else row_frag<RL, NORM, T3, false>(xa, xc, lds_ca, lds_cb, d0, inv1, bf, bl, rs);
         const int qa = (2 * ks + h) ^ csw;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -382,6 +357,15 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
             accl[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bl, accl[t], 0, 0, 0);
             accl[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bf, accl[t], 0, 0, 0);
           }
+#if RQSID_INTERLEAVE
+          const int g = ks * NT + t;
+#pragma unroll
+          for (int i = g * P / NG; i < (g + 1) * P / NG; ++i) {
+            RQSID_PIN_MFMA();
+            if (cn >= 0) issue_op(cn, i, true);
+            RQSID_PIN_MFMA();
+          }
+#endif
         }
       }
     };
@@ -391,29 +375,46 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
     for (int c = 0; c < S - 1; ++c)
       if (c < nch) issue(c);
     for (int c = 0; c < nch; ++c) {
+      ST(const uint64_t st_w0 = ST_NOW();)
       wait_chunks<S, P>(min(S - 2, nch - 1 - c));  // chunk c landed (every wave), chunk c-1 fully read
-      if (c + S - 1 < nch) issue(c + S - 1);         // into the stage chunk c-1 used
-      compute(c);
+      ST(st_wait += ST_NOW() - st_w0;)
+      const int cn = c + S - 1 < nch ? c + S - 1 : -1;  // into the stage chunk c-1 used
+#if !RQSID_INTERLEAVE
+      ST(const uint64_t st_i0 = ST_NOW();)
+      if (cn >= 0) issue(cn);
+      ST(st_issue += ST_NOW() - st_i0;)
+      compute(c, -1);
+#else
+      compute(c, cn);
+#endif
     }
 
+    ST(st_e0 = ST_NOW();)
     if (pass == 0) {
-      const float se2 = se2v.x + se2v.y, sf2 = sf2v.x + sf2v.y;
+      const float se2 = rs.se2v.x + rs.se2v.y, sf2 = rs.sf2v.x + rs.sf2v.y;
       const float e2 = se2 + __shfl_xor(se2, 32);
       en = sqrtf(e2) * 1.001f + 1e-30f;
       if (T3) {
-        const float l2 = se2l.x + se2l.y;
+        const float l2 = rs.se2l.x + rs.se2l.y;
         en2 = sqrtf(l2 + __shfl_xor(l2, 32)) * (1.001f / 4096.0f) + 1e-30f;
       }
       float nrm;
       if (NORM && RL >= 1) {
-        const double tot = sv2 + __shfl_xor(sv2, 32);
-        nrm = (float)sqrt(tot);
+        if (RL == 1) {  // exact: written to den_out
+          const double t2 = rs.sv2 + rs.sv2b;
+          nrm = (float)sqrt(t2 + __shfl_xor(t2, 32));
+        } else {  // fp32 sums: |nrm - |v|| <= den_eps |v| (chains of dim/4 + 2 terms, sqrt's half ulp)
+          nrm = sqrtf(sf2 + __shfl_xor(sf2, 32));
+        }
         const float den = nrm + 1e-8f;
         inv_den = 1.0f / den;
         if (RL == 1 && h == 0 && row_valid && p.den_out) p.den_out[my_row] = den;
         // |r_ref - v/den| per element: RL1: the reference rounds r_i = u_i/den once;
         // RL2: v was built with a reciprocal multiply (2 ulp of |r1| = 1) and rounded
-        dr = RL == 1 ? 2.0f * 5.97e-8f : (4.0f * 2.39e-7f * (1.0f + nrm) * inv_den + 4.0f * 5.97e-8f);
+        // RL2 also: the fp32 denominator's error, |v/den' - v/den| <= den_eps |v| / den'
+        const float den_eps = (0.125f * (float)(p.dim) + 3.0f) * 5.97e-8f;
+        dr = RL == 1 ? 2.0f * 5.97e-8f
+                     : (4.0f * 2.39e-7f * (1.0f + nrm) * inv_den + 4.0f * 5.97e-8f + 1.01f * den_eps * nrm * inv_den);
       } else {
         nrm = sqrtf(sf2 + __shfl_xor(sf2, 32));
       }
@@ -562,6 +563,15 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
       p.out_global[my_row] = cand_global(p, cbase, k);
     }
     push_work(p, h == 0 && row_valid && !definitive, lane, w);
+#ifdef RQSID_STAMPS
+    if (tid == 0) {
+      const uint64_t now = ST_NOW();
+      atomicAdd(&g_stamps_tile[0], (unsigned long long)(now - st_begin));
+      atomicAdd(&g_stamps_tile[1], (unsigned long long)st_wait);
+      atomicAdd(&g_stamps_tile[2], (unsigned long long)(now - st_e0));
+      atomicAdd(&g_stamps_tile[3], (unsigned long long)st_issue);
+    }
+#endif
     return;
   }
   // Row decision: keep the listed candidates still within the final U; a half that listed more
@@ -1042,6 +1052,14 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   else hipLaunchKernelGGL((assign_rescore_kernel<2, false>), g, dim3(256), 0, st, p);
   return check_launch("assign_rescore");
 }
+
+#ifdef RQSID_STAMPS
+int rqsid_debug_stamps_tile(unsigned long long* out4) {
+  if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_stamps_tile), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps_tile), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int rqsid_mfma_probe(int32_t f16, const uint16_t* a, const uint16_t* b, const float* c, float* d, void* stream) {
   if (!a || !b || !c || !d) return fail(RQSID_E_ARG, "mfma_probe: null argument");

@@ -163,6 +163,34 @@ __device__ __forceinline__ void dma16_nt(const void* gsrc, uint32_t lds_base) {
       : "memory");
 }
 
+// The same two without the memory clobber, for DMAs interleaved with a compute phase: they write a
+// ring stage no instruction of that phase reads (the barriers around the phase carry the ordering),
+// so hipcc may keep scheduling the phase's LDS reads across them.
+__device__ __forceinline__ void dma16_r(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base));
+}
+__device__ __forceinline__ void dma16_nt_r(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base));
+}
+// MFMAs stay on their side of this point; VALU, SALU and LDS reads may cross it
+#define RQSID_PIN_MFMA() __builtin_amdgcn_sched_barrier(0x0106)
+
 // wait until at most N of this wave's vector-memory ops are outstanding, drain LDS ops, barrier
 template <int N>
 __device__ __forceinline__ void wait_barrier() {
@@ -272,6 +300,158 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
   return v;
+}
+
+// diagnostic build only (-DRQSID_STAMPS): wave 0 of every block sums s_memtime cycles spent in the
+// kernel, in the chunk waits and in the epilogue into its file's g_stamps (tools/stamps.py)
+#ifdef RQSID_STAMPS
+#define ST_NOW() __builtin_amdgcn_s_memtime()
+#define ST(x) x
+#else
+#define ST(x)
+#endif
+
+#ifndef RQSID_PACKED_MAIN  // 1: the v_pk_* form of row_frag (A/B builds)
+#define RQSID_PACKED_MAIN 0
+#endif
+
+// Running sums of a row the screening bound needs (even / odd elements in .x / .y).
+struct RowSums {
+  f2 se2v = {0.f, 0.f};  // sum (v - fp16(v))^2
+  f2 se2l = {0.f, 0.f};  // T3: sum of the second term's residual^2 (units 2^-12)
+  f2 sf2v = {0.f, 0.f};  // sum v^2 in fp32 (the bound's |v|; RL 2 NORM: also the denominator, see kDenChain)
+  double sv2 = 0.0;      // RL 1 NORM: sum v^2 in fp64, even elements (den_out: the normalising denominator
+  double sv2b = 0.0;     // is exact), odd elements
+};
+// RL 1 NORM writes den = fl(sqrt(fp64 sum)) + 1e-8 to den_out (the next level's exact divisor).  RL 2 NORM
+// only screens with it: fp32 sums (chains of dim/4 + 2 terms), whose relative error the bound charges
+// (kDenRel, in units of 2^-24 per chain term, plus the sqrt's half ulp).
+constexpr bool fp64_norm(int rl, bool norm) { return norm && rl == 1; }
+
+// v - fp32(h): one v_fma_mix_f32 (the f16 operand converted inside the FMA, exact) instead of a
+// conversion and a subtraction
+template <int HI>
+__device__ __forceinline__ float sub_f16(float v, h2 hh) {
+  float d;
+  if (HI)
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d) : "v"(hh), "v"(v));
+  else
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[0,0,0] op_sel_hi:[1,0,0]" : "=v"(d) : "v"(hh), "v"(v));
+  return d;
+}
+
+// One 16-dim k-step of a row fragment: lane (r, h) holds dims d0 .. d0+7 of its row's vector
+//   RL 0: x,  1: x - ca,  2: (x - ca) [* inv1] - cb   (fp32 operation sequence of the reference)
+// as the MFMA B operand bf = fp16(v) [and bl = fp16((v - bf) 2^12), T3], adding to the bound's sums
+// when SUMS.  Scalar fp32: packed fp32 VALU (v_pk_*) issued beside MFMAs stalls the SIMD's matrix
+// pipe (MI355X_MICROARCH.md, 'price of one filler beside MFMAs'), and the compiler's SLP packing is
+// off for this library (-fno-slp-vectorize).  fp16 conversion is v_cvt_pk_f16_f32 (round to nearest
+// even; denormals flushed by the kernels' MODE, see to_f16); an input beyond the fp16 range becomes
+// inf, which makes the row's bound infinite -> exact re-score.
+template <int RL, bool NORM, bool T3, bool SUMS>
+__device__ __forceinline__ void row_frag(const float4 xa, const float4 xc, const float* lds_ca, const float* lds_cb,
+                                         int d0, float inv1, f16x8& bf, f16x8& bl, RowSums& s) {
+#if RQSID_PACKED_MAIN
+  f2 v[4] = {f2{xa.x, xa.y}, f2{xa.z, xa.w}, f2{xc.x, xc.y}, f2{xc.z, xc.w}};
+  if (RL >= 1) {
+    const float4 a0 = *reinterpret_cast<const float4*>(lds_ca + d0);
+    const float4 a1 = *reinterpret_cast<const float4*>(lds_ca + d0 + 4);
+    const f2 av[4] = {f2{a0.x, a0.y}, f2{a0.z, a0.w}, f2{a1.x, a1.y}, f2{a1.z, a1.w}};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] - av[e];
+  }
+  if (RL >= 2) {
+    const float4 b0 = *reinterpret_cast<const float4*>(lds_cb + d0);
+    const float4 b1 = *reinterpret_cast<const float4*>(lds_cb + d0 + 4);
+    const f2 bv[4] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1.x, b1.y}, f2{b1.z, b1.w}};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (NORM ? v[e] * inv1 : v[e]) - bv[e];
+  }
+  h2 hh[4], lh[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) hh[e] = __builtin_convertvector(v[e], h2);
+  bf = __builtin_shufflevector(__builtin_shufflevector(hh[0], hh[1], 0, 1, 2, 3),
+                               __builtin_shufflevector(hh[2], hh[3], 0, 1, 2, 3), 0, 1, 2, 3, 4, 5, 6, 7);
+  if (T3) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f2 xs = (v[e] - __builtin_convertvector(hh[e], f2)) * 4096.0f;  // exact
+      lh[e] = __builtin_convertvector(xs, h2);
+      if (SUMS) {
+        const f2 ev = xs - __builtin_convertvector(lh[e], f2);  // exact
+        s.se2l = ev * ev + s.se2l;
+      }
+    }
+    bl = __builtin_shufflevector(__builtin_shufflevector(lh[0], lh[1], 0, 1, 2, 3),
+                                 __builtin_shufflevector(lh[2], lh[3], 0, 1, 2, 3), 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+  if (SUMS) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f2 ex = v[e] - __builtin_convertvector(hh[e], f2);  // exact: the fp16 rounding residual
+      s.se2v = ex * ex + s.se2v;
+      if (fp64_norm(RL, NORM)) {
+        s.sv2 = fma((double)v[e].x, (double)v[e].x, s.sv2);
+        s.sv2b = fma((double)v[e].y, (double)v[e].y, s.sv2b);
+      } else {
+        s.sf2v = v[e] * v[e] + s.sf2v;
+      }
+    }
+  }
+#else
+  float v[8] = {xa.x, xa.y, xa.z, xa.w, xc.x, xc.y, xc.z, xc.w};
+  if (RL >= 1) {
+    const float4 a0 = *reinterpret_cast<const float4*>(lds_ca + d0);
+    const float4 a1 = *reinterpret_cast<const float4*>(lds_ca + d0 + 4);
+    const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = v[e] - a[e];  // exact fp32, as the reference
+  }
+  if (RL >= 2) {
+    const float4 b0 = *reinterpret_cast<const float4*>(lds_cb + d0);
+    const float4 b1 = *reinterpret_cast<const float4*>(lds_cb + d0 + 4);
+    const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (NORM ? v[e] * inv1 : v[e]) - b[e];
+  }
+  h2 hh[4], lh[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) hh[e] = __builtin_convertvector(f2{v[2 * e], v[2 * e + 1]}, h2);
+  bf = __builtin_shufflevector(__builtin_shufflevector(hh[0], hh[1], 0, 1, 2, 3),
+                               __builtin_shufflevector(hh[2], hh[3], 0, 1, 2, 3), 0, 1, 2, 3, 4, 5, 6, 7);
+  float ex[8];  // exact: the fp16 rounding residual
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ex[e] = (e & 1) ? sub_f16<1>(v[e], hh[e >> 1]) : sub_f16<0>(v[e], hh[e >> 1]);
+  if (T3) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lh[e] = __builtin_convertvector(f2{ex[2 * e] * 4096.0f, ex[2 * e + 1] * 4096.0f}, h2);
+    bl = __builtin_shufflevector(__builtin_shufflevector(lh[0], lh[1], 0, 1, 2, 3),
+                                 __builtin_shufflevector(lh[2], lh[3], 0, 1, 2, 3), 0, 1, 2, 3, 4, 5, 6, 7);
+    if (SUMS) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float ev = fmaf(ex[e], 4096.0f, -(float)lh[e >> 1][e & 1]);  // exact
+        if (e & 1) s.se2l.y = fmaf(ev, ev, s.se2l.y);
+        else s.se2l.x = fmaf(ev, ev, s.se2l.x);
+      }
+    }
+  }
+  if (SUMS) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (e & 1) s.se2v.y = fmaf(ex[e], ex[e], s.se2v.y);
+      else s.se2v.x = fmaf(ex[e], ex[e], s.se2v.x);
+      if (fp64_norm(RL, NORM)) {
+        if (e & 1) s.sv2b = fma((double)v[e], (double)v[e], s.sv2b);
+        else s.sv2 = fma((double)v[e], (double)v[e], s.sv2);
+      } else if (e & 1) {
+        s.sf2v.y = fmaf(v[e], v[e], s.sf2v.y);
+      } else {
+        s.sf2v.x = fmaf(v[e], v[e], s.sf2v.x);
+      }
+    }
+  }
+#endif
 }
 
 

@@ -19,32 +19,44 @@
 //    only make a later counted wait stronger, never weaker); a compaction pass lists them.
 #include "assign_common.h"
 
+#ifdef RQSID_STAMPS
+__device__ unsigned long long g_stamps[4];  // (diagnostic build, see assign_common.h)
+#endif
+
 namespace rqsid {
 namespace {
 
-constexpr int kSS = 3;                    // ring stages
 constexpr int kSC = 32;                   // dims per chunk (128-B row pieces: gathered rows stream at full rate)
 constexpr int kSDim = 512;                // the stream kernel's row width
 constexpr int kNch = kSDim / kSC;         // chunks per tile
-constexpr int kSW = 8;                    // waves per block
-constexpr int kSR = kSW * 32;             // rows per tile
-constexpr int kSX = kSR * kSC * 4;        // x stage: 256 rows x 128 B
 constexpr int kSentinel = -2;             // out_global of a row left to the re-score
 
-template <int NT, int RL, bool NORM, bool T3>
+// W waves per block (32 rows each), S ring stages.  Shapes: 8 x 3 (one block per CU) and 4 x 2 (two
+// blocks per CU: the other block's compute / epilogue covers this one's ring refill).
+template <int NT, int RL, bool NORM, bool T3, int W, int S>
 struct StreamLayout {
-  static constexpr int kCen = NT * 32 * kSC * 2;  // one fp16 centre table image: NT*32 x 64 B
+  static constexpr int kSR = W * 32;                              // rows per tile
+  static constexpr int kSX = kSR * kSC * 4;                       // x stage: kSR rows x 128 B
+  static constexpr int kCI = 2 * NT / W;                          // centre DMA ops per wave per table
+  static constexpr int kCen = NT * 32 * kSC * 2;                  // one fp16 centre table image: NT*32 x 64 B
   static constexpr int kStage = kSX + kCen * (T3 ? 2 : 1);
-  static constexpr int kRes = kSS * kStage;                    // [2 parities][RL rows] fp32 512
-  static constexpr int kSoa = kRes + 2 * RL * kSDim * 4;        // [2 parities][csq | y][NT*32] f32
-  static constexpr int kCidx = kSoa + 2 * 2 * NT * 32 * 4;      // [2 parities][NT*32] i32
-  static constexpr int kLand = kCidx + 2 * NT * 32 * 4;         // [8 waves][32] i32 (row idx, then den)
-  static constexpr int kBytes = kLand + kSW * 32 * 4;
-  static constexpr int P = 4 + (NT / 4) * (T3 ? 2 : 1);        // ring DMA ops per chunk per wave
-  static constexpr int E = 2 + (RL == 1 && NORM ? 1 : 0);       // fixed epilogue stores per wave
-  static constexpr int H1 = 2 + (RL >= 1 ? 1 : 0);              // header level-1 DMA ops per wave
-  static constexpr int H2 = 2 + (RL == 2 ? 1 : 0);              // header level-2 DMA ops per wave
-  static_assert(2 * P + E + H1 + H2 <= 63, "vmcnt field is 6 bits");
+  static constexpr int kRes = S * kStage;                         // [2 parities][RL rows] fp32 512
+  static constexpr int kSoa = kRes + 2 * RL * kSDim * 4;          // [2 parities][csq | y][NT*32] f32
+  static constexpr int kCidx = kSoa + 2 * 2 * NT * 32 * 4;        // [2 parities][NT*32] i32
+  static constexpr int kLand = kCidx + 2 * NT * 32 * 4;           // [W waves][32] i32 (row idx, then den)
+  static constexpr int kBytes = kLand + W * 32 * 4;
+  static constexpr int kBlocks = W == 8 ? 1 : 2;                  // blocks per CU
+  static constexpr int P = 4 + kCI * (T3 ? 2 : 1);                // ring DMA ops per chunk per wave
+  static constexpr int E = 2 + (RL == 1 && NORM ? 1 : 0);         // fixed epilogue stores per wave
+  static constexpr int H1 = 2 + (RL >= 1 ? 1 : 0);                // header level-1 DMA ops per wave
+  static constexpr int H2 = 2 + (RL == 2 ? 1 : 0);                // header level-2 DMA ops per wave
+  static constexpr int C1 = 2;                                    // chunk step issuing header level 1
+  static constexpr int C2 = C1 + S;                               // ... reading it, issuing level 2
+  static constexpr int C3 = C2 + S;                               // ... reading level 2
+  static_assert(S >= 2 && C3 < kNch, "header steps must fit one tile");
+  static_assert((2 * NT) % W == 0 && NT / 2 <= W && (RL < 2 || W >= 4), "header DMA: one op per wave");
+  static_assert((S - 1) * P + E + H1 + H2 <= 63, "vmcnt field is 6 bits");
+  static_assert(kBytes * kBlocks <= 160 * 1024, "LDS budget");
 };
 
 // one global_load_lds_dword: every lane moves 4 B from its own address to lds_base + lane*4
@@ -83,15 +95,16 @@ struct TileHdr {  // block-uniform (SGPRs)
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+template <int R>
 __device__ __forceinline__ TileHdr tile_header(const AssignParams& p, const int32_t* tile_seg,
-                                               const int32_t* seg_tile256, int T) {
+                                               const int32_t* seg_tiles, int T) {
   TileHdr H;
   H.T = T;
   H.s = uni(tile_seg[T]);
   const int s = H.s;
-  const int r0 = uni(p.seg_row_off[s]), r1 = uni(p.seg_row_off[s + 1]), tb = uni(seg_tile256[s]);
-  H.t0 = r0 + (T - tb) * kSR;
-  H.nrows = min(kSR, r1 - H.t0);
+  const int r0 = uni(p.seg_row_off[s]), r1 = uni(p.seg_row_off[s + 1]), tb = uni(seg_tiles[s]);
+  H.t0 = r0 + (T - tb) * R;
+  H.nrows = min(R, r1 - H.t0);
   H.cnt = uni(p.cand_count[s]);
   H.cbase = uni(p.cand_base[s]);
   H.flag = p.seg_flags && (uni(p.seg_flags[s]) & RQSID_SEG_PENALTY);
@@ -101,11 +114,12 @@ __device__ __forceinline__ TileHdr tile_header(const AssignParams& p, const int3
   return H;
 }
 
-template <int NT, int RL, bool NORM, bool T3>
-__global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, const int32_t* tile_seg,
-                                                              const int32_t* seg_tile256) {
-  using L = StreamLayout<NT, RL, NORM, T3>;
+template <int NT, int RL, bool NORM, bool T3, int W, int S>
+__global__ __launch_bounds__(W * 64, 2) void assign_stream_kernel(AssignParams p, const int32_t* tile_seg,
+                                                                 const int32_t* seg_tile256) {
+  using L = StreamLayout<NT, RL, NORM, T3, W, S>;
   constexpr int P = L::P;
+  constexpr int kSS = S, kSR = L::kSR, kSX = L::kSX, kCI = L::kCI;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #ifndef RQSID_AB_NO_FLUSH
   asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 6, 2), 0");  // fp16/fp64 denormals flushed (to_f16)
@@ -159,7 +173,7 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
   // (4 lanes per candidate): fragment-shaped (16-B-per-row) DMAs double the address-path work.
   struct Next {
     uint32_t xi[4];
-    uint32_t ci[NT / 4];
+    uint32_t ci[kCI];
     int my_row;
     float inv1;
   };
@@ -185,8 +199,8 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
     // centre image: candidate k at k*64 B, slot q stored at q ^ ((k>>2)&3); instruction j of wave w
     // moves candidates (w*NT/4 + j)*16 + lane/4, physical slot lane%4
 #pragma unroll
-    for (int j = 0; j < NT / 4; ++j) {
-      const int k = (wave * (NT / 4) + j) * 16 + (lane >> 2);
+    for (int j = 0; j < kCI; ++j) {
+      const int k = (wave * kCI + j) * 16 + (lane >> 2);
       const int sl = (lane & 3) ^ ((k >> 2) & 3);
       n.ci[j] = (uint32_t)cand_of(H, par, k) * 64u + (uint32_t)sl;
     }
@@ -218,17 +232,17 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
     for (int i = 0; i < 4; ++i) dma16_nt(addr(xb, n.xi[i]), uni(sb + wave * 4096 + i * 1024));
     const char* cb = cbase16 + c * (kSC * 2);
 #pragma unroll
-    for (int j = 0; j < NT / 4; ++j) dma16(addr(cb, n.ci[j]), uni(sb + kSX + (wave * (NT / 4) + j) * 1024));
+    for (int j = 0; j < kCI; ++j) dma16(addr(cb, n.ci[j]), uni(sb + kSX + (wave * kCI + j) * 1024));
     if (T3) {
       const char* cl = cb + lo_off * 2;
 #pragma unroll
-      for (int j = 0; j < NT / 4; ++j)
-        dma16(addr(cl, n.ci[j]), uni(sb + kSX + L::kCen + (wave * (NT / 4) + j) * 1024));
+      for (int j = 0; j < kCI; ++j)
+        dma16(addr(cl, n.ci[j]), uni(sb + kSX + L::kCen + (wave * kCI + j) * 1024));
     }
   };
 
   // ---- first tile: synchronous header --------------------------------------------------------
-  TileHdr Hc = tile_header(p, tile_seg, seg_tile256, T);
+  TileHdr Hc = tile_header<kSR>(p, tile_seg, seg_tile256, T);
   Next cur{};
   hdr_level1(Hc, 0);
   wait_barrier<0>();
@@ -243,6 +257,7 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
   bool first = true;
   int par = 0;
   int qb = 0;  // ring stage of this tile's chunk 0 (kNch % kSS != 0: the stage walks on across tiles)
+  ST(uint64_t st_wait = 0; uint64_t st_epi = 0; const uint64_t st_begin = ST_NOW();)
   for (;;) {
     const int Tn = T + G8;
     const bool more = Tn < xhi;
@@ -257,8 +272,7 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
     for (int t = 0; t < NT; ++t) acc[t] = zero16;
 #pragma unroll
     for (int t = 0; t < (T3 ? NT : 1); ++t) accl[t] = zero16;
-    double sv2 = 0.0;
-    f2 sf2v = {0.f, 0.f}, se2v = {0.f, 0.f}, se2l = {0.f, 0.f};
+    RowSums rs;
     const float* lds_ca = reinterpret_cast<const float*>(smem + L::kRes + (par * RL + 0) * kSDim * 4);
     const float* lds_cb = reinterpret_cast<const float*>(smem + L::kRes + (par * RL + (RL == 2 ? 1 : 0)) * kSDim * 4);
     const float inv1 = cur.inv1;
@@ -267,20 +281,23 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
 
 #pragma unroll 1
     for (int c = 0; c < kNch; ++c) {
-      // wait for chunk c: the younger ops are chunk c+1 and the groups issued after chunk c.  After
-      // the first tile, chunk 2 was issued at the start of the previous epilogue, before its E
-      // stores: c = 0 sees chunks 1, 2 + E, c = 1, 2 see one chunk + E.  Header level 1 (issued at
-      // c = 2) is younger than chunks 3, 4, level 2 (c = 5) than chunks 6, 7.  The barrier then also
-      // frees stage (c-1) % kSS.
-      if (more || c + 1 < kNch) {
-        if (!first && c == 0) wait_barrier<2 * P + L::E>();
-        else if (!first && c <= 2) wait_barrier<P + L::E>();
-        else if (c >= 3 && c <= 4 && more) wait_barrier<P + L::H1>();
-        else if (c >= 6 && c <= 7 && more) wait_barrier<P + L::H2>();
-        else wait_barrier<P>();
+      // wait for chunk c: the younger ops are chunks c+1 .. c+S-2 and the groups issued after chunk c.
+      // After the first tile, chunk S-1 was issued at the start of the previous epilogue, before its E
+      // stores: c = 0 sees chunks 1 .. S-1 + E, c = 1 .. S-1 see S-2 chunks + E.  Header level 1
+      // (issued at step C1) is younger than chunks C1+1 .. C1+S-1, level 2 (step C2) than chunks
+      // C2+1 .. C2+S-1.  The barrier then also frees stage (c-1) % S.
+      constexpr int YP = (S - 2) * P;  // the S-2 chunks issued after chunk c
+      ST(const uint64_t st_w0 = ST_NOW();)
+      if (more || c + S - 2 < kNch) {
+        if (!first && c == 0) wait_barrier<(S - 1) * P + L::E>();
+        else if (!first && c <= S - 1) wait_barrier<YP + L::E>();
+        else if (c > L::C1 && c <= L::C1 + S - 1 && more) wait_barrier<YP + L::H1>();
+        else if (c > L::C2 && c <= L::C2 + S - 1 && more) wait_barrier<YP + L::H2>();
+        else wait_barrier<YP>();
       } else {
         wait_barrier<0>();
       }
+      ST(st_wait += ST_NOW() - st_w0;)
       const int st = (qb + c) % kSS;
       if (c + kSS - 1 < kNch) {
         if (first || c != 0) issue(cur, c + kSS - 1, (qb + c + kSS - 1) % kSS);
@@ -301,7 +318,7 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
           if (p.seg_ca) w_ca = sload(p.seg_ca + sN);
           if (p.seg_cb) w_cbr = sload(p.seg_cb + sN);
         }
-        if (c == 2) {  // ... and this one the segment words
+        if (c == L::C1) {  // ... and this one the segment words
           SGPR_PIN(w_r0); SGPR_PIN(w_r1); SGPR_PIN(w_tb); SGPR_PIN(w_cnt);
           SGPR_PIN(w_cb); SGPR_PIN(w_fl); SGPR_PIN(w_ca); SGPR_PIN(w_cbr);
           Hn.T = Tn;
@@ -316,11 +333,11 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
           Hn.cb_row = p.seg_cb ? w_cbr : sN;
           hdr_level1(Hn, par ^ 1);
         }
-        if (c == 5) {
+        if (c == L::C2) {  // level 1 retired by this step's wait
           hdr_read1(Hn, par ^ 1, nxt);
           hdr_level2(Hn, par ^ 1, nxt);
         }
-        if (c == 8) hdr_read2(nxt);
+        if (c == L::C3) hdr_read2(nxt);
       }
 #if RQSID_AB_MODE < 3
       // compute chunk c (dims 32c .. 32c+31) in two k-steps: lane (r, h) owns row r of its wave and
@@ -331,52 +348,9 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
       const int q0 = 4 * ks + 2 * h;
       const float4 xa = *reinterpret_cast<const float4*>(xb + ((q0 ^ xsw) << 4));
       const float4 xc = *reinterpret_cast<const float4*>(xb + (((q0 + 1) ^ xsw) << 4));
-      f2 v[4] = {f2{xa.x, xa.y}, f2{xa.z, xa.w}, f2{xc.x, xc.y}, f2{xc.z, xc.w}};
       const int d0 = c * kSC + 16 * ks + 8 * h;
-      if (RL >= 1) {
-        const float4 a0 = *reinterpret_cast<const float4*>(lds_ca + d0);
-        const float4 a1 = *reinterpret_cast<const float4*>(lds_ca + d0 + 4);
-        const f2 av[4] = {f2{a0.x, a0.y}, f2{a0.z, a0.w}, f2{a1.x, a1.y}, f2{a1.z, a1.w}};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = v[e] - av[e];  // exact fp32, as the reference
-      }
-      if (RL >= 2) {
-        const float4 b0 = *reinterpret_cast<const float4*>(lds_cb + d0);
-        const float4 b1 = *reinterpret_cast<const float4*>(lds_cb + d0 + 4);
-        const f2 bv[4] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1.x, b1.y}, f2{b1.z, b1.w}};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (NORM ? v[e] * inv1 : v[e]) - bv[e];
-      }
-      h2 hh[4], lh[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) hh[e] = __builtin_convertvector(v[e], h2);
-      const f16x8 bf = __builtin_shufflevector(__builtin_shufflevector(hh[0], hh[1], 0, 1, 2, 3),
-                                               __builtin_shufflevector(hh[2], hh[3], 0, 1, 2, 3), 0, 1, 2, 3, 4, 5,
-                                               6, 7);
-      if (T3) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const f2 xs = (v[e] - __builtin_convertvector(hh[e], f2)) * 4096.0f;  // exact
-          lh[e] = __builtin_convertvector(xs, h2);
-          const f2 ev = xs - __builtin_convertvector(lh[e], f2);  // exact
-          se2l = ev * ev + se2l;
-        }
-      }
-      f16x8 bl = {};
-      if (T3)
-        bl = __builtin_shufflevector(__builtin_shufflevector(lh[0], lh[1], 0, 1, 2, 3),
-                                     __builtin_shufflevector(lh[2], lh[3], 0, 1, 2, 3), 0, 1, 2, 3, 4, 5, 6, 7);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const f2 ex = v[e] - __builtin_convertvector(hh[e], f2);  // exact: the fp16 rounding residual
-        se2v = ex * ex + se2v;
-        if (NORM && RL >= 1) {
-          sv2 = fma((double)v[e].x, (double)v[e].x, sv2);
-          sv2 = fma((double)v[e].y, (double)v[e].y, sv2);
-        } else {
-          sf2v = v[e] * v[e] + sf2v;
-        }
-      }
+      f16x8 bf, bl = {};
+      row_frag<RL, NORM, T3, true>(xa, xc, lds_ca, lds_cb, d0, inv1, bf, bl, rs);
       const unsigned char* cimg = smem + st * L::kStage + kSX + r * 64 + (((2 * ks + h) ^ csw) << 4);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -398,6 +372,7 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
 
     // the next tile's chunk 2 goes into chunk 15's stage as soon as every wave is done with it, so
     // three chunks stream during the epilogue (VALU only) instead of two
+    ST(const uint64_t st_e0 = ST_NOW();)
     if (more) {
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       issue(nxt, kSS - 1, (qb + kNch - 1) % kSS);
@@ -407,23 +382,30 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
     const int my_row = cur.my_row;
     float inv_den = 1.f, dr = 0.f, vn, en, en2 = 0.f;
     {
-      const float se2 = se2v.x + se2v.y, sf2 = sf2v.x + sf2v.y;
+      const float se2 = rs.se2v.x + rs.se2v.y, sf2 = rs.sf2v.x + rs.sf2v.y;
       en = sqrtf(se2 + __shfl_xor(se2, 32)) * 1.001f + 1e-30f;
       if (T3) {
-        const float l2 = se2l.x + se2l.y;
+        const float l2 = rs.se2l.x + rs.se2l.y;
         en2 = sqrtf(l2 + __shfl_xor(l2, 32)) * (1.001f / 4096.0f) + 1e-30f;
       }
       float nrm;
       if (NORM && RL >= 1) {
-        const double tot = sv2 + __shfl_xor(sv2, 32);
-        nrm = (float)sqrt(tot);
+        if (RL == 1) {  // exact: written to den_out
+          const double t2 = rs.sv2 + rs.sv2b;
+          nrm = (float)sqrt(t2 + __shfl_xor(t2, 32));
+        } else {  // fp32 sums: |nrm - |v|| <= den_eps |v| (chains of dim/4 + 2 terms, sqrt's half ulp)
+          nrm = sqrtf(sf2 + __shfl_xor(sf2, 32));
+        }
         const float den = nrm + 1e-8f;
         inv_den = 1.0f / den;
         if (RL == 1) {  // fixed-count store (dummy target for the other half / padding rows)
           float* dst = (h == 0 && row_valid) ? p.den_out + my_row : reinterpret_cast<float*>(dummy);
           *dst = den;
         }
-        dr = RL == 1 ? 2.0f * 5.97e-8f : (4.0f * 2.39e-7f * (1.0f + nrm) * inv_den + 4.0f * 5.97e-8f);
+        // RL2 also: the fp32 denominator's error, |v/den' - v/den| <= den_eps |v| / den'
+        const float den_eps = (0.125f * (float)(kSDim) + 3.0f) * 5.97e-8f;
+        dr = RL == 1 ? 2.0f * 5.97e-8f
+                     : (4.0f * 2.39e-7f * (1.0f + nrm) * inv_den + 4.0f * 5.97e-8f + 1.01f * den_eps * nrm * inv_den);
       } else {
         nrm = sqrtf(sf2 + __shfl_xor(sf2, 32));
       }
@@ -534,6 +516,7 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
     }
     if (need && h == 0 && row_valid) p.work[my_row] = w;  // may only strengthen the next counted waits
 
+    ST(st_epi += ST_NOW() - st_e0;)
     if (!more) break;
     T = Tn;
     Hc = Hn;
@@ -542,16 +525,24 @@ __global__ __launch_bounds__(512, 1) void assign_stream_kernel(AssignParams p, c
     qb = (qb + kNch) % kSS;
     first = false;
   }
+#ifdef RQSID_STAMPS
+  if (tid == 0) {
+    atomicAdd(&g_stamps[0], (unsigned long long)(ST_NOW() - st_begin));
+    atomicAdd(&g_stamps[1], (unsigned long long)st_wait);
+    atomicAdd(&g_stamps[2], (unsigned long long)st_epi);
+    atomicAdd(&g_stamps[3], 1ull);
+  }
+#endif
 }
 
 // 256-row tiling of the segments: seg_tile256[s] = sum_{s' < s} ceil(rows(s') / 256) (one block)
-__global__ __launch_bounds__(1024) void stream_tiles_kernel(const int32_t* __restrict__ seg_row_off, int nseg,
+__global__ __launch_bounds__(1024) void stream_tiles_kernel(const int32_t* __restrict__ seg_row_off, int nseg, int R,
                                                             int32_t* __restrict__ seg_tile256) {
   __shared__ int part[1024];
   const int tid = threadIdx.x;
   const int per = (nseg + 1023) / 1024, s0 = min(nseg, tid * per), s1 = min(nseg, s0 + per);
   int sum = 0;
-  for (int s = s0; s < s1; ++s) sum += (seg_row_off[s + 1] - seg_row_off[s] + kSR - 1) / kSR;
+  for (int s = s0; s < s1; ++s) sum += (seg_row_off[s + 1] - seg_row_off[s] + R - 1) / R;
   part[tid] = sum;
   __syncthreads();
   for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
@@ -563,7 +554,7 @@ __global__ __launch_bounds__(1024) void stream_tiles_kernel(const int32_t* __res
   int run = part[tid] - sum;
   for (int s = s0; s < s1; ++s) {
     seg_tile256[s] = run;
-    run += (seg_row_off[s + 1] - seg_row_off[s] + kSR - 1) / kSR;
+    run += (seg_row_off[s + 1] - seg_row_off[s] + R - 1) / R;
   }
   if (tid == 1023) seg_tile256[nseg] = part[1023];
 }
@@ -582,10 +573,10 @@ __global__ __launch_bounds__(256) void tile_seg_kernel(const int32_t* __restrict
   }
 }
 
-template <int NT, int RL, bool NORM, bool T3>
-bool launch_one(const AssignParams& p, const int32_t* tile_seg, const int32_t* seg_tile256, int64_t max_tiles,
+template <int NT, int RL, bool NORM, bool T3, int W, int S>
+bool launch_one(const AssignParams& p, const int32_t* tile_seg, const int32_t* seg_tiles, int64_t max_tiles,
                 hipStream_t st) {
-  using L = StreamLayout<NT, RL, NORM, T3>;
+  using L = StreamLayout<NT, RL, NORM, T3, W, S>;
   static int ncu = 0;
   static bool attr = false;
   if (!ncu) {
@@ -595,36 +586,36 @@ bool launch_one(const AssignParams& p, const int32_t* tile_seg, const int32_t* s
     ncu = prop.multiProcessorCount;
   }
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)assign_stream_kernel<NT, RL, NORM, T3>,
+    if (hipFuncSetAttribute((const void*)assign_stream_kernel<NT, RL, NORM, T3, W, S>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, L::kBytes) != hipSuccess)
       return false;
     attr = true;
   }
-  int64_t g = ncu;  // one 8-wave block per CU
+  int64_t g = (int64_t)ncu * L::kBlocks;  // persistent: every block resident at once
   if (g > max_tiles) g = max_tiles;
   g = g / 8 * 8;
   if (g < 8) g = 8;
-  hipLaunchKernelGGL((assign_stream_kernel<NT, RL, NORM, T3>), dim3((unsigned)g), dim3(kSW * 64), L::kBytes, st, p,
-                     tile_seg, seg_tile256);
+  hipLaunchKernelGGL((assign_stream_kernel<NT, RL, NORM, T3, W, S>), dim3((unsigned)g), dim3(W * 64), L::kBytes, st,
+                     p, tile_seg, seg_tiles);
   return true;
 }
 
-}  // namespace
-
-bool stream_supported(int nt, bool t3, int rl, bool norm) {
-  (void)norm;
-  if (nt == 8) return !t3 && rl >= 0 && rl <= 2;
-  if (nt == 4) return rl >= 0 && rl <= 2;
-  return false;
+// block shape: RQSID_STREAM_SHAPE = 83 (8 waves x 3 stages, the default) or 42 (4 waves x 2 stages)
+int stream_shape() {
+  const char* e = getenv("RQSID_STREAM_SHAPE");
+  const int v = e ? atoi(e) : 83;
+  return v == 42 ? 42 : 83;
 }
 
-void launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
-                          int32_t* seg_tile256, int64_t cap, hipStream_t st) {
-  hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, seg_tile256);
-  const int64_t max_tiles = cap / kSR + p.n_segments;  // bound on the 256-row tiles
+template <int W, int S>
+void launch_shape(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles,
+                  int64_t cap, hipStream_t st) {
+  constexpr int R = W * 32;
+  hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, R, seg_tiles);
+  const int64_t max_tiles = cap / R + p.n_segments;  // bound on the R-row tiles
   const unsigned tg = (unsigned)(max_tiles / 256 + 1 < 4096 ? max_tiles / 256 + 1 : 4096);
-  hipLaunchKernelGGL(tile_seg_kernel, dim3(tg), dim3(256), 0, st, seg_tile256, p.n_segments, cap, tile_seg);
-#define RQ_L(NT, RL, NORM, T3) launch_one<NT, RL, NORM, T3>(p, tile_seg, seg_tile256, max_tiles, st)
+  hipLaunchKernelGGL(tile_seg_kernel, dim3(tg), dim3(256), 0, st, seg_tiles, p.n_segments, cap, tile_seg);
+#define RQ_L(NT, RL, NORM, T3) launch_one<NT, RL, NORM, T3, W, S>(p, tile_seg, seg_tiles, max_tiles, st)
   if (nt == 8) {
     if (rl == 0) RQ_L(8, 0, false, false);
     else if (rl == 1) { if (norm) RQ_L(8, 1, true, false); else RQ_L(8, 1, false, false); }
@@ -641,4 +632,27 @@ void launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool n
 #undef RQ_L
 }
 
+}  // namespace
+
+bool stream_supported(int nt, bool t3, int rl, bool norm) {
+  (void)norm;
+  if (nt == 8) return !t3 && rl >= 0 && rl <= 2;
+  if (nt == 4) return rl >= 0 && rl <= 2;
+  return false;
+}
+
+void launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
+                          int32_t* seg_tiles, int64_t cap, hipStream_t st) {
+  if (stream_shape() == 42) launch_shape<4, 2>(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
+  else launch_shape<8, 3>(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
+}
+
 }  // namespace rqsid
+
+#ifdef RQSID_STAMPS
+extern "C" int rqsid_debug_stamps(unsigned long long* out4) {
+  if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_stamps), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -386,3 +386,20 @@ def test_stream_nearest_partial_tiles(k):
     assert (got == tile).all()
     sel = np.arange(0, 30000, 29)
     assert (got[sel] == exact_ids(x[sel], c)).all()
+
+
+def test_integration_md_binding_runs():
+    """The ctypes stub INTEGRATION.md shows a maintainer (KMeans.predict's argmin through the C ABI)
+    runs against the built library and returns the exact argmin."""
+    import re
+    from pathlib import Path
+    from generative_ranking_recommender_amd import _lib
+    text = (Path(__file__).resolve().parent.parent / "INTEGRATION.md").read_text()
+    code = re.search(r"```python\n(# balancekmeans/_rqsid.py.*?)```", text, re.S).group(1)
+    code = code.replace('"/path/to/generative_ranking_recommender_amd/librqsid.so"', repr(str(_lib.LIB_PATH)))
+    ns = {}
+    exec(compile(code, "INTEGRATION.md", "exec"), ns)
+    x = synth.small_mixture(3000, d=512, m=50, seed=5)
+    c = synth.small_mixture(128, d=512, m=50, seed=6)
+    got = ns["nearest_center"](torch.from_numpy(x), torch.from_numpy(c)).numpy()
+    assert (got == exact_ids(x, c)).all()

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Diagnostics (GPU, stamps build: tools/ab_build.sh with EXTRA=-DRQSID_STAMPS): per encode level, the
+screen kernel's (stream or per-tile) wave-0 cycles per block split into chunk waits, epilogue and the rest."""
+import ctypes
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import bench  # noqa: E402
+from generative_ranking_recommender_amd import _lib, ops  # noqa: E402
+import generative_ranking_recommender_amd.encode as encmod  # noqa: E402
+from generative_ranking_recommender_amd.encode import HIERARCHICAL_TRAIN, RQEncoder  # noqa: E402
+
+
+def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000))):
+    dev = torch.device("cuda", 0)
+    z = np.load(os.environ["SWEEP_CB"])
+    cb = {k: z[k] for k in z.files}
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], [128, 128, 256],
+                    match=torch.from_numpy(cb["match"]), semantics=HIERARCHICAL_TRAIN, device=dev)
+    x = bench.make_rows(n, 0, dev)
+    lib = _lib.load()
+    fn = lib.rqsid_debug_stamps if os.environ.get("RQSID_SCREEN_VARIANT") == "5" else lib.rqsid_debug_stamps_tile
+    fn.argtypes = [ctypes.c_void_p]
+    buf = (ctypes.c_ulonglong * 4)()
+    enc.encode(x)
+    torch.cuda.synchronize()
+    fn(buf)
+    orig = ops.assign
+    res = []
+
+    def hook(*a, **k):
+        out = orig(*a, **k)
+        torch.cuda.synchronize()
+        fn(buf)
+        res.append(list(buf))
+        return out
+
+    encmod.ops.assign = hook
+    enc.encode(x)
+    stream = os.environ.get("RQSID_SCREEN_VARIANT") == "5"
+    for lvl, (tot, wt, ep, x) in enumerate(res):
+        # stream kernel: x = blocks; per-tile kernel: x = cycles in the ring's DMA issue
+        iss = 0 if stream else x
+        print(f"L{lvl}: cycles {tot:.4g}  wait {100 * wt / max(tot, 1):.1f}%  epilogue {100 * ep / max(tot, 1):.1f}%  "
+              f"dma issue {100 * iss / max(tot, 1):.1f}%  rest {100 * (tot - wt - ep - iss) / max(tot, 1):.1f}%", flush=True)
+
+
+if __name__ == "__main__":
+    main()
