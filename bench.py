@@ -52,7 +52,24 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--codebooks", choices=("fitted", "sampled"), default=os.environ.get("BENCH_CODEBOOKS", "fitted"),
                     help="fitted: short K-Means fits on a sample (trained-model geometry); sampled: residual rows")
+    ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "r1_traffic.json"),
+                    help="PMC HBM bytes per launch of this build (tools/pmc_traffic.sh); missing file -> traffic null")
     return ap.parse_args()
+
+
+# kernels of each encode level's rqsid_assign call (per-tile screen + exact re-score; see encode.py)
+LEVEL_KERNELS = {0: ("assign_screen_kernel<4, 2, 0, false, false, true>", "assign_rescore_kernel<0, false>"),
+                 1: ("assign_screen_kernel<4, 2, 1, true, true, true>", "assign_rescore_kernel<1, true>"),
+                 2: ("assign_screen_kernel<8, 2, 2, true, false, true>", "assign_rescore_kernel<2, true>")}
+
+
+def level_traffic(path, lvl):
+    """HBM bytes (PMC FETCH_SIZE x2 + WRITE_SIZE) of one launch of level lvl's kernels, or None."""
+    try:
+        ks = json.load(open(path))["kernels"]
+        return sum(ks[k]["hbm_bytes"] for k in LEVEL_KERNELS[lvl])
+    except (OSError, KeyError, TypeError, ValueError):
+        return None
 
 
 class Timed:
@@ -244,9 +261,13 @@ def main():
         kern["bucket"] = {"ms": round(ms["bucket"], 3)}
     dom = max((k for k in kern if k.startswith("assign")), key=lambda k: kern[k]["ms"])
     dk = kern[dom]
+    traffic = level_traffic(args.traffic_json, int(dom[-1])) if os.environ.get("RQSID_SCREEN_VARIANT", "0") == "0" else None
     roof = {"kernel": dom + " (rqsid_assign: assign_screen_kernel + assign_rescore_kernel)", "bound": "hbm",
             "achieved": dk["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dk["hbm_frac"],
-            "traffic": None, "bytes_per_row": bytes_row}
+            "traffic": traffic, "traffic_unit": "bytes per launch",
+            "traffic_source": (os.path.relpath(args.traffic_json, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+                               "separate passes, same build and workload)") if traffic else None,
+            "algorithmic_bytes": n * bytes_row, "bytes_per_row": bytes_row}
 
     total_rows = n * world * args.steps
     value = total_rows / elapsed
@@ -262,7 +283,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic Gaussian mixture (4096 blobs, sigma 0.25) generated on device; synthetic residual codebooks",
+        "data": "synthetic Gaussian mixture (4096 blobs, sigma 0.25) generated on device; " +
+                ("PROD-shaped codebooks fitted on a 1M-row sample (short Lloyd fits, random init)" if args.codebooks == "fitted"
+                 else "PROD-shaped codebooks sampled from residual rows"),
         "config": {"workload": f"3-level RQ encode, {n} x {D} fp32 rows per GPU, need [128,128,256], "
                                "layer_clusters [128,1280,1280] (BASELINE configs[2]/[3])",
                    "rows_per_gpu": n, "dim": D, "need_clusters": NEED, "candidates_last_level": N_CAND,

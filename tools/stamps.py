@@ -26,7 +26,7 @@ def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000))):
     lib = _lib.load()
     fn = lib.rqsid_debug_stamps if os.environ.get("RQSID_SCREEN_VARIANT") == "5" else lib.rqsid_debug_stamps_tile
     fn.argtypes = [ctypes.c_void_p]
-    buf = (ctypes.c_ulonglong * 4)()
+    buf = (ctypes.c_ulonglong * 8)()
     enc.encode(x)
     torch.cuda.synchronize()
     fn(buf)
@@ -43,11 +43,12 @@ def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000))):
     encmod.ops.assign = hook
     enc.encode(x)
     stream = os.environ.get("RQSID_SCREEN_VARIANT") == "5"
-    for lvl, (tot, wt, ep, x) in enumerate(res):
-        # stream kernel: x = blocks; per-tile kernel: x = cycles in the ring's DMA issue
-        iss = 0 if stream else x
-        print(f"L{lvl}: cycles {tot:.4g}  wait {100 * wt / max(tot, 1):.1f}%  epilogue {100 * ep / max(tot, 1):.1f}%  "
-              f"dma issue {100 * iss / max(tot, 1):.1f}%  rest {100 * (tot - wt - ep - iss) / max(tot, 1):.1f}%", flush=True)
+    for lvl, (tot, wt, ep, x, pro, *_) in enumerate(res):
+        # x = cycles in the ring's DMA issue; pro = per-tile prologue (stream kernel: next-header steps)
+        iss = x
+        f = lambda v: f"{100 * v / max(tot, 1):.1f}%"
+        print(f"L{lvl}: cycles {tot:.4g}  prologue {f(pro)}  wait {f(wt)}  dma issue {f(iss)}  epilogue {f(ep)}  "
+              f"compute {f(tot - wt - ep - iss - pro)}", flush=True)
 
 
 if __name__ == "__main__":
