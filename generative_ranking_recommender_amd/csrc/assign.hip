@@ -135,7 +135,7 @@ struct ScreenLayout {
 // ub = P + E / lb = P - E (lb overwrites the accumulator) and half a min3 (sweep 1), then a compare
 // and two selects (sweep 2: how many candidates have lb <= U, the last two of them).
 #ifdef RQSID_STAMPS
-__device__ unsigned long long g_stamps_tile[4];
+__device__ unsigned long long g_stamps_tile[8];
 #endif
 
 template <int NT, int S, int RL, bool NORM, bool T3, bool ONE>
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, r = lane & 31;
-  ST(const uint64_t st_begin = ST_NOW(); uint64_t st_wait = 0; uint64_t st_e0 = 0; uint64_t st_issue = 0;)
+  ST(const uint64_t st_begin = ST_NOW(); uint64_t st_wait = 0; uint64_t st_e0 = 0; uint64_t st_issue = 0; uint64_t st_ring = 0;)
   // XCD-aware tile order: blocks b and b+8 share an XCD (and its L2), so give each group of 8 a
   // contiguous run of tiles -> a segment's candidate centres stay hot in one L2 (gridDim.x % 8 == 0)
   const int G = gridDim.x;
@@ -200,20 +200,23 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
     const int slot = (lane & 7) ^ ((rr >> 1) & 7);
     xsrc[i] = p.x + (int64_t)grow * dim + slot * 4;
   }
-  // residual rows of this segment -> LDS
+  // residual rows of this segment -> LDS (staged below, after the ring's first DMAs are in flight)
   float* lds_ca = reinterpret_cast<float*>(smem + L::kRes);
   float* lds_cb = lds_ca + dim;
-  if (RL >= 1) {
-    const float4* a = reinterpret_cast<const float4*>(p.ca + (int64_t)seg_row(p.seg_ca, s) * dim);
-    for (int i = tid; i < dim / 4; i += 256) reinterpret_cast<float4*>(lds_ca)[i] = a[i];
-  }
-  if (RL >= 2) {
-    const float4* a = reinterpret_cast<const float4*>(p.cb + (int64_t)seg_row(p.seg_cb, s) * dim);
-    for (int i = tid; i < dim / 4; i += 256) reinterpret_cast<float4*>(lds_cb)[i] = a[i];
-  }
   float inv1 = 1.0f;
-  if (RL >= 2 && NORM) inv1 = 1.0f / p.den_in[my_row];
-  asm volatile("" : "+v"(inv1));  // its load completes before the DMA ring starts
+  auto stage_residual_rows = [&]() {
+    if (RL >= 1) {
+      const float4* a = reinterpret_cast<const float4*>(p.ca + (int64_t)seg_row(p.seg_ca, s) * dim);
+      for (int i = tid; i < dim / 4; i += 256) reinterpret_cast<float4*>(lds_ca)[i] = a[i];
+    }
+    if (RL >= 2) {
+      const float4* a = reinterpret_cast<const float4*>(p.cb + (int64_t)seg_row(p.seg_cb, s) * dim);
+      for (int i = tid; i < dim / 4; i += 256) reinterpret_cast<float4*>(lds_cb)[i] = a[i];
+    }
+    if (RL >= 2 && NORM) inv1 = 1.0f / p.den_in[my_row];
+    asm volatile("" : "+v"(inv1));  // its load completes before the ring's compute starts
+  };
+  if (!ONE) stage_residual_rows();
 
   const uint32_t lds0 = lds_addr(smem);
   const int nch = dim / kChunk;
@@ -256,7 +259,40 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
 #endif
       if (T3) clo[j] = csrc[j] + (int64_t)p.n_centers * dim;
     }
-    __syncthreads();
+#ifdef RQSID_AB_CMAJOR
+    const int64_t kCStride = (int64_t)p.n_centers * kChunk;
+#else
+    constexpr int kCStride = kChunk;
+#endif
+    // DMA op i of chunk c (x rows 0..3, hi centres, lo centres) into stage c % S
+    auto issue_op = [&](int c, int i, bool relaxed) {
+      const uint32_t sb = lds0 + (uint32_t)((c % S) * L::kStage);
+      if (i < 4) {
+        const void* src = xsrc[i] + c * kChunk;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(sb + wave * kXWaveBytes + i * 1024);
+        if (relaxed) dma16_nt_r(src, dst); else dma16_nt(src, dst);
+      } else {
+        const int j = (i - 4) % (NT / 2), lo = (i - 4) / (NT / 2);
+        const void* src = (lo ? clo[T3 ? j : 0] : csrc[j]) + c * kCStride;
+        const uint32_t dst =
+            __builtin_amdgcn_readfirstlane(sb + kXStage + lo * L::kCHalf + (wave * (NT / 2) + j) * 1024);
+        if (relaxed) dma16_r(src, dst); else dma16(src, dst);
+      }
+    };
+    auto issue = [&](int c) {
+#pragma unroll
+      for (int i = 0; i < P; ++i) issue_op(c, i, false);
+    };
+    if constexpr (ONE) {
+      // single pass: the ring's first chunks go out before the tile's remaining header work (residual
+      // rows, candidate meta), whose loads then overlap their flight; the barrier below drains both
+#pragma unroll
+      for (int c = 0; c < S - 1; ++c)
+        if (c < nch) issue(c);
+      stage_residual_rows();
+    } else {
+      __syncthreads();
+    }
     if constexpr (ONE) {
       float gz = 0.f, gw = 0.f, gy = 0.f;
       if (tid < NT * 32) {
@@ -298,30 +334,6 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
 #pragma unroll
     for (int t = 0; t < (T3 ? NT : 1); ++t) accl[t] = zero16;
 
-#ifdef RQSID_AB_CMAJOR
-    const int64_t kCStride = (int64_t)p.n_centers * kChunk;
-#else
-    constexpr int kCStride = kChunk;
-#endif
-    // DMA op i of chunk c (x rows 0..3, hi centres, lo centres) into stage c % S
-    auto issue_op = [&](int c, int i, bool relaxed) {
-      const uint32_t sb = lds0 + (uint32_t)((c % S) * L::kStage);
-      if (i < 4) {
-        const void* src = xsrc[i] + c * kChunk;
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(sb + wave * kXWaveBytes + i * 1024);
-        if (relaxed) dma16_nt_r(src, dst); else dma16_nt(src, dst);
-      } else {
-        const int j = (i - 4) % (NT / 2), lo = (i - 4) / (NT / 2);
-        const void* src = (lo ? clo[T3 ? j : 0] : csrc[j]) + c * kCStride;
-        const uint32_t dst =
-            __builtin_amdgcn_readfirstlane(sb + kXStage + lo * L::kCHalf + (wave * (NT / 2) + j) * 1024);
-        if (relaxed) dma16_r(src, dst); else dma16(src, dst);
-      }
-    };
-    auto issue = [&](int c) {
-#pragma unroll
-      for (int i = 0; i < P; ++i) issue_op(c, i, false);
-    };
     // compute chunk c; the P DMA ops of chunk cn (< 0: none) are spread between its 2*NT MFMA groups,
     // so a DMA issue stall (the load path's back-pressure) overlaps MFMAs in flight instead of
     // preceding the whole phase
@@ -370,10 +382,13 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
       }
     };
 
-    // S-stage ring: chunks 0..S-2 in flight before the first compute
+    ST(st_ring = ST_NOW();)
+    // S-stage ring: chunks 0..S-2 in flight before the first compute (single pass: issued above)
+    if (!ONE) {
 #pragma unroll
-    for (int c = 0; c < S - 1; ++c)
-      if (c < nch) issue(c);
+      for (int c = 0; c < S - 1; ++c)
+        if (c < nch) issue(c);
+    }
     for (int c = 0; c < nch; ++c) {
       ST(const uint64_t st_w0 = ST_NOW();)
       wait_chunks<S, P>(min(S - 2, nch - 1 - c));  // chunk c landed (every wave), chunk c-1 fully read
@@ -570,6 +585,7 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
       atomicAdd(&g_stamps_tile[1], (unsigned long long)st_wait);
       atomicAdd(&g_stamps_tile[2], (unsigned long long)(now - st_e0));
       atomicAdd(&g_stamps_tile[3], (unsigned long long)st_issue);
+      atomicAdd(&g_stamps_tile[4], (unsigned long long)(st_ring - st_begin));
     }
 #endif
     return;
@@ -1054,9 +1070,9 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
 }
 
 #ifdef RQSID_STAMPS
-int rqsid_debug_stamps_tile(unsigned long long* out4) {
-  if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_stamps_tile), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
-  const unsigned long long z[4] = {0, 0, 0, 0};
+int rqsid_debug_stamps_tile(unsigned long long* out8) {
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stamps_tile), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps_tile), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -20,7 +20,7 @@
 #include "assign_common.h"
 
 #ifdef RQSID_STAMPS
-__device__ unsigned long long g_stamps[4];  // (diagnostic build, see assign_common.h)
+__device__ unsigned long long g_stamps[8];  // (diagnostic build, see assign_common.h)
 #endif
 
 namespace rqsid {
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(W * 64, 2) void assign_stream_kernel(AssignParams p
   bool first = true;
   int par = 0;
   int qb = 0;  // ring stage of this tile's chunk 0 (kNch % kSS != 0: the stage walks on across tiles)
-  ST(uint64_t st_wait = 0; uint64_t st_epi = 0; const uint64_t st_begin = ST_NOW();)
+  ST(uint64_t st_wait = 0; uint64_t st_epi = 0; uint64_t st_issue = 0; uint64_t st_hdr = 0; const uint64_t st_begin = ST_NOW();)
   for (;;) {
     const int Tn = T + G8;
     const bool more = Tn < xhi;
@@ -299,11 +299,13 @@ __global__ __launch_bounds__(W * 64, 2) void assign_stream_kernel(AssignParams p
       }
       ST(st_wait += ST_NOW() - st_w0;)
       const int st = (qb + c) % kSS;
+      ST(const uint64_t st_i0 = ST_NOW();)
       if (c + kSS - 1 < kNch) {
         if (first || c != 0) issue(cur, c + kSS - 1, (qb + c + kSS - 1) % kSS);
       } else if (more) {
         issue(nxt, c + kSS - 1 - kNch, (qb + c + kSS - 1) % kSS);
       }
+      ST(const uint64_t st_h0 = ST_NOW(); st_issue += st_h0 - st_i0;)
       if (more) {
         if (c == 0) sN = sload(tile_seg + Tn);
         if (c == 1) {  // this iteration's wait_barrier retired the tile_seg load (lgkmcnt(0))
@@ -339,6 +341,7 @@ __global__ __launch_bounds__(W * 64, 2) void assign_stream_kernel(AssignParams p
         }
         if (c == L::C3) hdr_read2(nxt);
       }
+      ST(st_hdr += ST_NOW() - st_h0;)
 #if RQSID_AB_MODE < 3
       // compute chunk c (dims 32c .. 32c+31) in two k-steps: lane (r, h) owns row r of its wave and
       // dims 32c + 16ks + 8h + 0..7 (the per-tile kernel's fragment layout)
@@ -530,7 +533,560 @@ __global__ __launch_bounds__(W * 64, 2) void assign_stream_kernel(AssignParams p
     atomicAdd(&g_stamps[0], (unsigned long long)(ST_NOW() - st_begin));
     atomicAdd(&g_stamps[1], (unsigned long long)st_wait);
     atomicAdd(&g_stamps[2], (unsigned long long)st_epi);
-    atomicAdd(&g_stamps[3], 1ull);
+    atomicAdd(&g_stamps[3], (unsigned long long)st_issue);
+    atomicAdd(&g_stamps[4], (unsigned long long)st_hdr);
+  }
+#endif
+}
+
+// ---- ping-pong form: the 8 waves of the block are two 4-wave groups (waves 0-3: rows 0-127 of the
+// 256-row tile, waves 4-7: rows 128-255; one wave of each group per SIMD) that alternate roles every
+// phase: while one group runs the MFMAs of chunk j, the other issues its share of the ring's DMAs
+// (and the next tile's header loads).  The compute waves never stall on DMA issue (140-200 cycles per
+// global_load_lds_dwordx4 under load, tools/stamps.py), and each SIMD runs one computing wave at a
+// time.  Phases are barrier-separated; chunk j's centre image is shared by both groups (group 0
+// computes it in phase 2j, group 1 in phase 2j+1).
+//   phase 2j   : group 0 computes chunk j;   group 1 issues the centres of chunk j+1 and its rows of j+2
+//   phase 2j+1 : group 1 computes chunk j;   group 0 issues its rows of chunk j+3
+// (rows stream three chunks ahead from HBM, the L2-resident centres one).  Chunk numbers continue across
+// tiles (16.. = the next tile's 0..).  LDS: rows [2 groups][3 stages] x 16 KiB, centres [2 stages].
+// Group 0 runs its epilogue in phase 31 (after its issue), group 1 in the next tile's phase 0 (after
+// its issue); both while the other group computes.
+template <int NT, int RL, bool NORM, bool T3>
+struct PPLayout {
+  static constexpr int kCI = NT / 2;                       // centre DMA ops per group-1 wave per table
+  static constexpr int kCen = NT * 32 * kSC * 2;           // one fp16 table image of a chunk
+  static constexpr int kCStage = kCen * (T3 ? 2 : 1);
+  static constexpr int kXG = 128 * kSC * 4;                // one group's rows of a chunk: 16 KiB
+  static constexpr int kX = 0;                             // [2 groups][3 stages]
+  static constexpr int kC = kX + 6 * kXG;                  // [2 stages]
+  static constexpr int kRes = kC + 2 * kCStage;            // [2 parities][RL rows] fp32 512
+  static constexpr int kSoa = kRes + 2 * RL * kSDim * 4;
+  static constexpr int kCidx = kSoa + 2 * 2 * NT * 32 * 4;
+  static constexpr int kLand = kCidx + 2 * NT * 32 * 4;
+  static constexpr int kBytes = kLand + 8 * 32 * 4;
+  static constexpr int PC = kCI * (T3 ? 2 : 1);            // centre ops per group-1 wave per chunk
+  static constexpr int E = 2 + (RL == 1 && NORM ? 1 : 0);
+  static constexpr int H1 = 2 + (RL >= 1 ? 1 : 0);
+  static constexpr int H2 = 2 + (RL == 2 ? 1 : 0);
+  static constexpr int C1 = 2, C2 = 6, C3 = 10;            // header steps (their phases: see the waits)
+  static_assert(kBytes <= 160 * 1024, "LDS budget");
+  static_assert(2 * (PC + 4) + E + H1 + H2 <= 63, "vmcnt field is 6 bits");
+};
+
+// Scalar loads that complete inside the asm (s_waitcnt lgkmcnt(0) before it returns): their outputs
+// are valid SGPRs at once, so hipcc may copy or spill them freely (the ping-pong kernel's header
+// steps sit in several inlined phase copies, where an asynchronous load's output would be copied
+// before it lands).
+__device__ __forceinline__ uint64_t uni64(const void* ptr) {
+  const uint64_t a = reinterpret_cast<uint64_t>(ptr);
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a);
+}
+__device__ __forceinline__ int sload_now(const void* ptr) {
+  int v;
+  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(uni64(ptr)) : "memory");
+  return v;
+}
+struct SegWords {
+  int r0, r1, tb, cnt, cb, fl, ca, cbr;
+};
+// segment s's header words (seg_row_off[s], [s+1], seg_tiles[s], cand_count[s], cand_base[s], the
+// aligned seg_flags word holding byte s, seg_ca[s], seg_cb[s]; absent arrays read a harmless word)
+__device__ __forceinline__ SegWords seg_words(const AssignParams& p, const int32_t* seg_tiles, int s) {
+  const void* fl = p.seg_flags ? reinterpret_cast<const void*>(reinterpret_cast<uintptr_t>(p.seg_flags + s) & ~(uintptr_t)3)
+                               : (const void*)p.seg_row_off;
+  const void* ca = p.seg_ca ? (const void*)(p.seg_ca + s) : (const void*)p.seg_row_off;
+  const void* cb = p.seg_cb ? (const void*)(p.seg_cb + s) : (const void*)p.seg_row_off;
+  SegWords w;
+  asm volatile(
+      "s_load_dword %0, %8, 0x0\n\t"
+      "s_load_dword %1, %8, 0x4\n\t"
+      "s_load_dword %2, %9, 0x0\n\t"
+      "s_load_dword %3, %10, 0x0\n\t"
+      "s_load_dword %4, %11, 0x0\n\t"
+      "s_load_dword %5, %12, 0x0\n\t"
+      "s_load_dword %6, %13, 0x0\n\t"
+      "s_load_dword %7, %14, 0x0\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&s"(w.r0), "=&s"(w.r1), "=&s"(w.tb), "=&s"(w.cnt), "=&s"(w.cb), "=&s"(w.fl),
+        "=&s"(w.ca), "=&s"(w.cbr)
+      : "s"(uni64(p.seg_row_off + s)), "s"(uni64(seg_tiles + s)), "s"(uni64(p.cand_count + s)),
+        "s"(uni64(p.cand_base + s)), "s"(uni64(fl)), "s"(uni64(ca)), "s"(uni64(cb))
+      : "memory");
+  return w;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+__device__ __forceinline__ void lgkm_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int NT, int RL, bool NORM, bool T3>
+__global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const int32_t* tile_seg,
+                                                           const int32_t* seg_tile256) {
+  using L = PPLayout<NT, RL, NORM, T3>;
+  constexpr int PC = L::PC, kCI = L::kCI, kSR = 256;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#ifndef RQSID_AB_NO_FLUSH
+  asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 6, 2), 0");  // fp16/fp64 denormals flushed (to_f16)
+#endif
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = uni(tid >> 6);
+  const int grp = wave >> 2, gw = wave & 3;
+  const int h = lane >> 5, r = lane & 31;
+  const uint32_t lds0 = lds_addr(smem);
+
+  const int ntiles = uni(seg_tile256[p.n_segments]);
+  const int G8 = (int)(gridDim.x >> 3), xcd = (int)(blockIdx.x & 7), slot = (int)(blockIdx.x >> 3);
+  const int xlo = (int)((int64_t)xcd * ntiles / 8), xhi = (int)((int64_t)(xcd + 1) * ntiles / 8);
+  int T = xlo + slot;
+  if (T >= xhi) return;
+
+  // table-wide bound constants (meta row k)
+  const float* trow = p.c_meta + 4 * (int64_t)p.n_centers;
+  const float tscale = __uint_as_float(uni(__float_as_uint(trow[0])));
+  const float tgz = __uint_as_float(uni(__float_as_uint(trow[1])));
+  const float tgw = __uint_as_float(uni(__float_as_uint(trow[2])));
+  const float tgy = __uint_as_float(uni(__float_as_uint(trow[3])));
+  const int64_t lo_off = (int64_t)p.n_centers * kSDim;  // T3: the lo table follows the hi table
+  int* const dummy = p.work_count + 16;                 // sink of the fixed-count stores
+
+  // ---- header pipeline pieces -------------------------------------------------------------
+  // level 1: row indices (wave w: rows 32w..32w+31, lanes 0..31), candidate indices (wave w:
+  // candidates (w % (NT/2))*64 + lane; later waves repeat), residual centre rows (RL >= 1)
+  auto hdr_level1 = [&](const TileHdr& H, int par) {
+    const int lr = min(32 * wave + r, H.nrows - 1);
+    if (lane < 32)  // (exec-masked: still one vector-memory op of this wave)
+      dma4(p.row_index ? (const void*)(p.row_index + H.t0 + lr) : (const void*)p.seg_row_off,
+           uni(lds0 + L::kLand + wave * 128));
+    const int k = (wave % (NT / 2)) * 64 + lane;
+    const int kc = H.cnt > 0 ? min(k, H.cnt - 1) : 0;
+    dma4(p.cand_idx && H.cnt > 0 ? (const void*)(p.cand_idx + H.cbase + kc) : (const void*)p.seg_row_off,
+         uni(lds0 + L::kCidx + par * NT * 128 + (wave % (NT / 2)) * 256));
+    if (RL >= 1) {  // RL1: ca halves by wave parity; RL2: waves w%4 = 0,1 ca, 2,3 cb (the rest repeat)
+      const int half = wave & 1;
+      const bool second = RL == 2 && (wave & 2);
+      const float* src = second ? p.cb + (int64_t)H.cb_row * kSDim : p.ca + (int64_t)H.ca_row * kSDim;
+      dma16(src + half * 256 + lane * 4,
+            uni(lds0 + L::kRes + (par * RL + (second ? 1 : 0)) * kSDim * 4 + half * 1024));
+    }
+  };
+  // read level 1 (after the barrier that retires it): this wave's row ids and DMA sources of the tile
+  // DMA sources as 32-bit indices of 16-B units (row*128 + slot, candidate*64 + slot): the 64-bit
+  // address is one v_mad_u64_u32 per DMA, and a tile's sources cost 4 + NT/4 VGPRs, not twice that.
+  // Every DMA instruction moves whole 128-B row lines (8 lanes per row) or 64-B candidate pieces
+  // (4 lanes per candidate): fragment-shaped (16-B-per-row) DMAs double the address-path work.
+  struct Next {
+    uint32_t xi[4];
+    uint32_t ci[kCI];
+    int my_row;
+    float inv1;
+  };
+  auto cand_of = [&](const TileHdr& H, int par, int k) -> int {  // global centre of local candidate k
+    if (H.pen) return 0;
+    if (!p.cand_idx) return H.cbase + min(k, H.cnt - 1);
+    return reinterpret_cast<const int*>(smem + L::kCidx + par * NT * 128)[min(k, NT * 32 - 1)];
+  };
+  auto hdr_read1 = [&](const TileHdr& H, int par, Next& n) {
+    const int* land = reinterpret_cast<const int*>(smem + L::kLand + wave * 128);
+    auto row_of = [&](int lr) {  // lr: row within this wave's 32
+      return p.row_index ? land[lr] : H.t0 + min(32 * wave + lr, H.nrows - 1);
+    };
+    n.my_row = row_of(r);
+    // x image of wave w (4 KiB per stage): row rr at rr*128 B, 16-B slot q stored at q ^ ((rr>>1)&7)
+    // (conflict-free fragment reads); instruction i moves rows 8i + lane/8, physical slot lane%8
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int lr = 8 * i + (lane >> 3);
+      const int sl = (lane & 7) ^ ((lr >> 1) & 7);
+      n.xi[i] = (uint32_t)row_of(lr) * 128u + (uint32_t)sl;
+    }
+    // centre image: candidate k at k*64 B, slot q stored at q ^ ((k>>2)&3); instruction j of wave w
+    // moves candidates (w*NT/4 + j)*16 + lane/4, physical slot lane%4
+#pragma unroll
+    for (int j = 0; j < kCI; ++j) {
+      const int k = (gw * kCI + j) * 16 + (lane >> 2);
+      const int sl = (lane & 3) ^ ((k >> 2) & 3);
+      n.ci[j] = (uint32_t)cand_of(H, par, k) * 64u + (uint32_t)sl;
+    }
+  };
+  // level 2: |c|^2 and |c| of the candidates (SoA, gathered from meta), den_in of the rows (RL2 NORM)
+  auto hdr_level2 = [&](const TileHdr& H, int par, const Next& n) {
+    const int k = (wave % (NT / 2)) * 64 + lane;
+    const float* m = p.c_meta + 4 * (int64_t)cand_of(H, par, k);
+    dma4(m, uni(lds0 + L::kSoa + (par * 2 + 0) * NT * 128 + (wave % (NT / 2)) * 256));
+    dma4(m + 1, uni(lds0 + L::kSoa + (par * 2 + 1) * NT * 128 + (wave % (NT / 2)) * 256));
+    if (RL == 2 && lane < 32)
+      dma4(NORM ? (const void*)(p.den_in + n.my_row) : (const void*)p.seg_row_off, uni(lds0 + L::kLand + wave * 128));
+  };
+  auto hdr_read2 = [&](Next& n) {
+    if (RL == 2 && NORM) n.inv1 = 1.0f / reinterpret_cast<const float*>(smem + L::kLand + wave * 128)[r];
+    else n.inv1 = 1.0f;
+  };
+
+  // ---- ring: this wave's share of chunk j (tile-relative; 16, 17 = the next tile's 0, 1) ----------
+  const char* const xbase = reinterpret_cast<const char*>(p.x);
+  const char* const cbase16 = reinterpret_cast<const char*>(p.c16);
+  auto addr = [](const char* base, uint32_t unit) -> const void* { return base + (uint64_t)unit * 16u; };
+  int qb = 0;  // row stage of this tile's chunk 0 (16 % 3 != 0: walks on across tiles)
+  auto issue_c = [&](const Next& n, int j) __attribute__((always_inline)) {  // group 1: chunk j's centres
+    const uint32_t sc = lds0 + L::kC + (j & 1) * L::kCStage;
+    const char* cb = cbase16 + (j & 15) * (kSC * 2);
+#pragma unroll
+    for (int q = 0; q < kCI; ++q) dma16(addr(cb, n.ci[q]), uni(sc + (gw * kCI + q) * 1024));
+    if (T3) {
+      const char* cl = cb + lo_off * 2;
+#pragma unroll
+      for (int q = 0; q < kCI; ++q) dma16(addr(cl, n.ci[q]), uni(sc + L::kCen + (gw * kCI + q) * 1024));
+    }
+  };
+  auto issue_x = [&](const Next& n, int j) __attribute__((always_inline)) {  // this group's rows of chunk j
+    const uint32_t sx = lds0 + L::kX + (grp * 3 + (qb + j) % 3) * L::kXG + gw * 4096;
+    const char* xb = xbase + (j & 15) * (kSC * 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma16_nt(addr(xb, n.xi[i]), uni(sx + i * 1024));
+  };
+
+  // ---- first tile: synchronous header ----------------------------------------------------------
+  TileHdr Hc = tile_header<kSR>(p, tile_seg, seg_tile256, T);
+  Next cur{};
+  hdr_level1(Hc, 0);
+  wait_barrier<0>();
+  hdr_read1(Hc, 0, cur);
+  hdr_level2(Hc, 0, cur);
+  wait_barrier<0>();
+  hdr_read2(cur);
+  if (grp == 0) {
+    issue_x(cur, 0);
+    issue_x(cur, 1);
+    issue_x(cur, 2);
+  } else {
+    issue_x(cur, 0);
+    issue_c(cur, 0);
+    issue_x(cur, 1);
+  }
+
+  const f32x16 zero16 = {};
+  f32x16 acc[NT];
+  f32x16 accl[T3 ? NT : 1];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = zero16;
+#pragma unroll
+  for (int t = 0; t < (T3 ? NT : 1); ++t) accl[t] = zero16;
+  RowSums rs;
+  const int xsw = (r >> 1) & 7;  // x image swizzle of this lane's row
+  const int csw = (r >> 2) & 3;  // centre image swizzle of this lane's candidate rows
+  int par = 0;
+  bool first = true;
+  ST(uint64_t st_wait = 0; uint64_t st_comp = 0; uint64_t st_epi = 0; const uint64_t st_begin = ST_NOW();)
+  TileHdr Hp{};  // group 1: the tile whose epilogue is still pending
+  int row_p = 0, par_p = 0;
+
+  auto epilogue = [&](const TileHdr& H_, int my_row_, int par_) __attribute__((always_inline)) {
+      const bool row_valid = 32 * wave + r < H_.nrows;
+      const int my_row = my_row_;
+      float inv_den = 1.f, dr = 0.f, vn, en, en2 = 0.f;
+      {
+        const float se2 = rs.se2v.x + rs.se2v.y, sf2 = rs.sf2v.x + rs.sf2v.y;
+        en = sqrtf(se2 + __shfl_xor(se2, 32)) * 1.001f + 1e-30f;
+        if (T3) {
+          const float l2 = rs.se2l.x + rs.se2l.y;
+          en2 = sqrtf(l2 + __shfl_xor(l2, 32)) * (1.001f / 4096.0f) + 1e-30f;
+        }
+        float nrm;
+        if (NORM && RL >= 1) {
+          if (RL == 1) {  // exact: written to den_out
+            const double t2 = rs.sv2 + rs.sv2b;
+            nrm = (float)sqrt(t2 + __shfl_xor(t2, 32));
+          } else {  // fp32 sums: |nrm - |v|| <= den_eps |v| (chains of dim/4 + 2 terms, sqrt's half ulp)
+            nrm = sqrtf(sf2 + __shfl_xor(sf2, 32));
+          }
+          const float den = nrm + 1e-8f;
+          inv_den = 1.0f / den;
+          if (RL == 1) {  // fixed-count store (dummy target for the other half / padding rows)
+            float* dst = (h == 0 && row_valid) ? p.den_out + my_row : reinterpret_cast<float*>(dummy);
+            *dst = den;
+          }
+          // RL2 also: the fp32 denominator's error, |v/den' - v/den| <= den_eps |v| / den'
+          const float den_eps = (0.125f * (float)(kSDim) + 3.0f) * 5.97e-8f;
+          dr = RL == 1 ? 2.0f * 5.97e-8f
+                       : (4.0f * 2.39e-7f * (1.0f + nrm) * inv_den + 4.0f * 5.97e-8f + 1.01f * den_eps * nrm * inv_den);
+        } else {
+          nrm = sqrtf(sf2 + __shfl_xor(sf2, 32));
+        }
+        vn = nrm * 1.0001f + 1e-30f;
+      }
+      int out_l = kSentinel, out_g = kSentinel;
+      bool need = false;
+      WorkItem w{};
+      w.row = my_row;
+      w.seg = H_.s;
+      if (H_.pen) {
+        need = true;
+        w.n = H_.flag ? -2 : -3;
+      } else {
+  #if RQSID_AB_MODE >= 1
+        float sink = 0.f;
+  #pragma unroll
+        for (int t = 0; t < NT; ++t)
+  #pragma unroll
+          for (int v = 0; v < 16; ++v) sink += acc[t][v] + (T3 ? accl[T3 ? t : 0][v] : 0.f);
+        const int k = sink == -1.2345e38f ? 1 : (int)(((uint32_t)my_row * 2654435761u) >> 8) % H_.cnt;
+        out_l = p.cand_lid ? 0 : k;
+        out_g = cand_of(Hc, par_, k);
+  #else
+        const float hn = vn + en;
+        const float vr = vn * inv_den;
+        const float ar = p.acc_rel, ar2 = 2.0f * p.acc_rel, k2 = 2.0f * inv_den * 1.000001f;
+        const float A = T3 ? k2 * (en2 + ar * hn + ar2 * (en + en2)) + 2.0f * dr + 7.2e-7f * vr
+                           : k2 * (en + ar * hn) + 2.0f * dr + 4.8e-7f * vr;
+        const float B = T3 ? k2 * (hn * (1.0f + ar2) + 2.0f * (en + en2)) : k2 * hn * (1.0f + ar);
+        const float C = T3 ? k2 * ((en + en2) + ar * hn + ar2 * (hn + en + en2)) : 0.0f;
+        const float m2 = -2.0f * inv_den * tscale;
+        const float A2 = (A + B * (T3 ? tgz : tgw) + C * tgw + 2.39e-7f * tgy) * 1.000001f;
+        const f2 m2v = {m2, m2}, a2v = {A2, A2}, epsv = {1e-30f, 1e-30f};
+        const float* m_csq = reinterpret_cast<const float*>(smem + L::kSoa + (par_ * 2 + 0) * NT * 128);
+        const float* m_y = reinterpret_cast<const float*>(smem + L::kSoa + (par_ * 2 + 1) * NT * 128);
+        float U = INFINITY;
+  #pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          __builtin_amdgcn_sched_barrier(0);
+  #pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float4 csq = *reinterpret_cast<const float4*>(m_csq + t * 32 + 8 * g + 4 * h);
+            const float4 yy = *reinterpret_cast<const float4*>(m_y + t * 32 + 8 * g + 4 * h);
+  #pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const int v = 4 * g + 2 * e;
+              f2 d = {acc[t][v], acc[t][v + 1]};
+              if (T3) d = f2{accl[T3 ? t : 0][v], accl[T3 ? t : 0][v + 1]} * 0x1p-12f + d;
+              const f2 P2 = m2v * d + (e ? f2{csq.z, csq.w} : f2{csq.x, csq.y});
+              const f2 E2 = a2v * (e ? f2{yy.z, yy.w} : f2{yy.x, yy.y}) + epsv;
+              const f2 ub = P2 + E2, lb = P2 - E2;
+              U = fminf(U, fminf(ub.x, ub.y));
+              acc[t][v] = lb.x;
+              acc[t][v + 1] = lb.y;
+            }
+          }
+        }
+        U = fminf(U, __shfl_xor(U, 32));
+        const float Up = fmaf(fabsf(U), 0x1p-22f, U) + 1.2e-38f;
+        const f2 upv = {Up, Up};
+        uint32_t pbits[NT / 2];
+  #pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          __builtin_amdgcn_sched_barrier(0);
+          uint32_t b = (t & 1) ? pbits[t >> 1] : 0u;
+  #pragma unroll
+          for (int v = 0; v < 16; v += 2) {
+            const f2 d = f2{acc[t][v], acc[t][v + 1]} - upv;
+            b = __builtin_amdgcn_alignbit(b, __float_as_uint(d.x), 31);
+            b = __builtin_amdgcn_alignbit(b, __float_as_uint(d.y), 31);
+          }
+          pbits[t >> 1] = b;
+        }
+        // candidates beyond cnt (duplicates of the last one) never pass
+        // (a lane half's candidates ascend with v, so a tile's valid values are a prefix of its 16 bits)
+        if (H_.cnt < NT * 32) {
+  #pragma unroll
+          for (int wd = 0; wd < NT / 2; ++wd) {
+            uint32_t m = 0;
+  #pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int rem = H_.cnt - 32 * (2 * wd + q) - 4 * h;  // valid iff (v&3) + 8(v>>2) < rem
+              int nv = 0;
+  #pragma unroll
+              for (int g = 0; g < 4; ++g) nv += min(4, max(0, rem - 8 * g));
+              const uint32_t pre = (uint32_t)((0xFFFFull << (16 - nv)) & 0xFFFFull);
+              m |= q == 0 ? pre << 16 : pre;
+            }
+            pbits[wd] &= m;
+          }
+        }
+        int k = -1;
+        if (pass_decide(pbits, h, k, w)) {
+          out_l = k;
+          out_g = cand_of(Hc, par_, k);
+        } else {
+          need = true;
+        }
+  #endif
+      }
+      {  // fixed-count output stores: exactly E per wave whatever the rows decided
+        const bool mine = h == 0 && row_valid;
+        int* dl = mine ? p.out_local + my_row : dummy;
+        int* dg = mine ? p.out_global + my_row : dummy;
+        *dl = out_l;
+        *dg = out_g;
+      }
+      if (need && h == 0 && row_valid) p.work[my_row] = w;  // may only strengthen the next counted waits
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = zero16;
+#pragma unroll
+    for (int t = 0; t < (T3 ? NT : 1); ++t) accl[t] = zero16;
+    rs = RowSums{};
+  };
+
+  for (;;) {
+    const int Tn = T + G8;
+    const bool more = Tn < xhi;
+    TileHdr Hn{};
+    Next nxt{};
+    int sN = 0, w_r0 = 0, w_r1 = 0, w_tb = 0, w_cnt = 0, w_cb = 0, w_fl = 0, w_ca = 0, w_cbr = 0;
+    const float* lds_ca = reinterpret_cast<const float*>(smem + L::kRes + (par * RL + 0) * kSDim * 4);
+    const float* lds_cb = reinterpret_cast<const float*>(smem + L::kRes + (par * RL + (RL == 2 ? 1 : 0)) * kSDim * 4);
+    const float inv1 = cur.inv1;
+    // header steps of this group's load phases: s = 0 tile_seg, 1 segment words, 2 level 1, 5 level 2, 8 read 2
+    auto header_step = [&](int s) __attribute__((always_inline)) {
+      if (!more) return;
+      if (s == 0) sN = sload_now(tile_seg + Tn);
+      if (s == 1) {
+        const SegWords sw = seg_words(p, seg_tile256, sN);
+        w_r0 = sw.r0; w_r1 = sw.r1; w_tb = sw.tb; w_cnt = sw.cnt;
+        w_cb = sw.cb; w_fl = sw.fl; w_ca = sw.ca; w_cbr = sw.cbr;
+      }
+      if (s == L::C1) {
+        Hn.T = Tn;
+        Hn.s = sN;
+        Hn.t0 = w_r0 + (Tn - w_tb) * kSR;
+        Hn.nrows = min(kSR, w_r1 - Hn.t0);
+        Hn.cnt = w_cnt;
+        Hn.cbase = w_cb;
+        Hn.flag = p.seg_flags && ((w_fl >> (8 * (sN & 3))) & RQSID_SEG_PENALTY);
+        Hn.pen = Hn.flag || Hn.cnt <= 0;
+        Hn.ca_row = p.seg_ca ? w_ca : sN;
+        Hn.cb_row = p.seg_cb ? w_cbr : sN;
+        hdr_level1(Hn, par ^ 1);
+      }
+      if (s == L::C2) {  // level 1 of both groups retired and barrier-ordered
+        hdr_read1(Hn, par ^ 1, nxt);
+        hdr_level2(Hn, par ^ 1, nxt);
+      }
+      if (s == L::C3) hdr_read2(nxt);
+    };
+    auto compute = [&](int j) __attribute__((always_inline)) {
+#if RQSID_AB_MODE < 3
+      const unsigned char* xrow = smem + L::kX + (grp * 3 + (qb + j) % 3) * L::kXG + (32 * gw + r) * 128;
+      const unsigned char* cimg0 = smem + L::kC + (j & 1) * L::kCStage + r * 64;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int q0 = 4 * ks + 2 * h;
+        const float4 xa = *reinterpret_cast<const float4*>(xrow + ((q0 ^ xsw) << 4));
+        const float4 xc = *reinterpret_cast<const float4*>(xrow + (((q0 + 1) ^ xsw) << 4));
+        const int d0 = j * kSC + 16 * ks + 8 * h;
+        f16x8 bf, bl = {};
+        row_frag<RL, NORM, T3, true>(xa, xc, lds_ca, lds_cb, d0, inv1, bf, bl, rs);
+        const unsigned char* cimg = cimg0 + (((2 * ks + h) ^ csw) << 4);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const f16x8 af = *reinterpret_cast<const f16x8*>(cimg + t * 32 * 64);
+#if RQSID_AB_MODE >= 2
+          acc[t][0] += (float)bf[0] + (float)af[0];
+#else
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[t], 0, 0, 0);
+          if (T3) {
+            const f16x8 al = *reinterpret_cast<const f16x8*>(cimg + L::kCen + t * 32 * 64);
+            accl[T3 ? t : 0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bl, accl[T3 ? t : 0], 0, 0, 0);
+            accl[T3 ? t : 0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bf, accl[T3 ? t : 0], 0, 0, 0);
+          }
+#endif
+        }
+      }
+#endif
+    };
+
+    // counted waits (ops per wave, in issue order; group 1 issues centres before rows, headers and the
+    // epilogue's E stores come last in a phase): see the schedule above
+    auto phase_even = [&](int j) __attribute__((always_inline)) {
+      // ---- phase 2j: group 0 computes chunk j; group 1 issues centres(j+1), rows(j+2) ------------------
+      const bool tail = !more && j >= 12;  // no next-tile traffic: the counted waits below would be too weak
+      ST(const uint64_t st_w0 = ST_NOW();)
+      if (tail) wait_vm<0>();
+      else if (grp == 0) {  // rows(j): phase 2j-5; younger: rows(j+1), rows(j+2) [+ E, header]
+        if (!first && j <= 2) wait_vm<8 + L::E>();
+        else if (more && (j == 3 || j == 4)) wait_vm<8 + L::H1>();
+        else if (more && (j == 7 || j == 8)) wait_vm<8 + L::H2>();
+        else wait_vm<8>();
+      } else {  // centres(j): phase 2j-2; younger: rows(j+1) [+ E, header]
+        if (!first && j == 1) wait_vm<4 + L::E>();
+        else if (more && j == 4) wait_vm<4 + L::H1>();
+        else if (more && j == 8) wait_vm<4 + L::H2>();
+        else wait_vm<4>();
+      }
+      lgkm_barrier();
+      ST(const uint64_t st_w1 = ST_NOW(); st_wait += st_w1 - st_w0;)
+      if (grp == 0) {
+        compute(j);
+        ST(st_comp += ST_NOW() - st_w1;)
+      } else {
+        if (j + 1 < kNch) issue_c(cur, j + 1);
+        else if (more) issue_c(nxt, j + 1);
+        if (j + 2 < kNch) issue_x(cur, j + 2);
+        else if (more) issue_x(nxt, j + 2);
+        if (j >= 1) header_step(j - 1);
+      }
+    };
+    auto phase_odd = [&](int j) __attribute__((always_inline)) {
+      // ---- phase 2j+1: group 1 computes chunk j; group 0 issues rows(j+3) -------------------------------
+      const bool tail = !more && j >= 12;
+      ST(const uint64_t st_w0 = ST_NOW();)
+      if (grp == 1) {  // rows(j): phase 2j-4; younger: phases 2j-2, 2j [+ E, header]
+        if (tail) wait_vm<0>();
+        else if (!first && j <= 1) wait_vm<2 * (PC + 4) + L::E>();
+        else if (more && (j == 3 || j == 4)) wait_vm<2 * (PC + 4) + L::H1>();
+        else if (more && (j == 7 || j == 8)) wait_vm<2 * (PC + 4) + L::H2>();
+        else wait_vm<2 * (PC + 4)>();
+      }
+      lgkm_barrier();
+      ST(const uint64_t st_w1 = ST_NOW(); st_wait += st_w1 - st_w0;)
+      if (grp == 1) {
+        compute(j);
+        ST(st_comp += ST_NOW() - st_w1;)
+      } else {
+        if (j + 3 < kNch) issue_x(cur, j + 3);
+        else if (more) issue_x(nxt, j + 3);
+        header_step(j);
+      }
+    };
+    // chunk 0 and chunk 15 are peeled: the epilogues run outside the chunk loop (register pressure)
+    phase_even(0);
+    ST(const uint64_t st_e0 = ST_NOW();)
+    if (grp == 1 && !first) epilogue(Hp, row_p, par_p);  // the previous tile's, after this phase's issue
+    ST(st_epi += ST_NOW() - st_e0;)
+    phase_odd(0);
+#pragma unroll 1
+    for (int j = 1; j < kNch - 1; ++j) {
+      phase_even(j);
+      phase_odd(j);
+    }
+    phase_even(kNch - 1);
+    phase_odd(kNch - 1);
+    ST(const uint64_t st_e1 = ST_NOW();)
+    if (grp == 0) epilogue(Hc, cur.my_row, par);  // after this phase's issue, while group 1 computes
+    ST(st_epi += ST_NOW() - st_e1;)
+    if (grp == 1) {
+      Hp = Hc;
+      row_p = cur.my_row;
+      par_p = par;
+    }
+    if (!more) break;
+    T = Tn;
+    Hc = Hn;
+    cur = nxt;
+    par ^= 1;
+    qb = (qb + kNch) % 3;
+    first = false;
+  }
+  if (grp == 1) epilogue(Hp, row_p, par_p);  // the last tile
+#ifdef RQSID_STAMPS
+  if (lane == 0 && (wave == 0 || wave == 4)) {
+    const int o = wave == 0 ? 0 : 4;
+    atomicAdd(&g_stamps[o + 0], (unsigned long long)(ST_NOW() - st_begin));
+    atomicAdd(&g_stamps[o + 1], (unsigned long long)st_wait);
+    atomicAdd(&g_stamps[o + 2], (unsigned long long)st_comp);
+    atomicAdd(&g_stamps[o + 3], (unsigned long long)st_epi);
   }
 #endif
 }
@@ -600,11 +1156,63 @@ bool launch_one(const AssignParams& p, const int32_t* tile_seg, const int32_t* s
   return true;
 }
 
-// block shape: RQSID_STREAM_SHAPE = 83 (8 waves x 3 stages, the default) or 42 (4 waves x 2 stages)
+// block shape: RQSID_STREAM_SHAPE = 83 (8 waves x 3 stages, the default), 42 (4 waves x 2 stages) or
+// 88 (the ping-pong 8-wave form)
 int stream_shape() {
   const char* e = getenv("RQSID_STREAM_SHAPE");
   const int v = e ? atoi(e) : 83;
-  return v == 42 ? 42 : 83;
+  return v == 42 || v == 88 ? v : 83;
+}
+
+template <int NT, int RL, bool NORM, bool T3>
+bool launch_pp(const AssignParams& p, const int32_t* tile_seg, const int32_t* seg_tiles, int64_t max_tiles,
+               hipStream_t st) {
+  using L = PPLayout<NT, RL, NORM, T3>;
+  static int ncu = 0;
+  static bool attr = false;
+  if (!ncu) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+    ncu = prop.multiProcessorCount;
+  }
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)assign_pp_kernel<NT, RL, NORM, T3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            L::kBytes) != hipSuccess)
+      return false;
+    attr = true;
+  }
+  int64_t g = ncu;  // one persistent 8-wave block per CU
+  if (g > max_tiles) g = max_tiles;
+  g = g / 8 * 8;
+  if (g < 8) g = 8;
+  hipLaunchKernelGGL((assign_pp_kernel<NT, RL, NORM, T3>), dim3((unsigned)g), dim3(512), L::kBytes, st, p, tile_seg,
+                     seg_tiles);
+  return true;
+}
+
+void launch_pp_shape(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles,
+                     int64_t cap, hipStream_t st) {
+  constexpr int R = 256;
+  hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, R, seg_tiles);
+  const int64_t max_tiles = cap / R + p.n_segments;
+  const unsigned tg = (unsigned)(max_tiles / 256 + 1 < 4096 ? max_tiles / 256 + 1 : 4096);
+  hipLaunchKernelGGL(tile_seg_kernel, dim3(tg), dim3(256), 0, st, seg_tiles, p.n_segments, cap, tile_seg);
+#define RQ_L(NT, RL, NORM, T3) launch_pp<NT, RL, NORM, T3>(p, tile_seg, seg_tiles, max_tiles, st)
+  if (nt == 8) {
+    if (rl == 0) RQ_L(8, 0, false, false);
+    else if (rl == 1) { if (norm) RQ_L(8, 1, true, false); else RQ_L(8, 1, false, false); }
+    else { if (norm) RQ_L(8, 2, true, false); else RQ_L(8, 2, false, false); }
+  } else if (t3) {
+    if (rl == 0) RQ_L(4, 0, false, true);
+    else if (rl == 1) { if (norm) RQ_L(4, 1, true, true); else RQ_L(4, 1, false, true); }
+    else { if (norm) RQ_L(4, 2, true, true); else RQ_L(4, 2, false, true); }
+  } else {
+    if (rl == 0) RQ_L(4, 0, false, false);
+    else if (rl == 1) { if (norm) RQ_L(4, 1, true, false); else RQ_L(4, 1, false, false); }
+    else { if (norm) RQ_L(4, 2, true, false); else RQ_L(4, 2, false, false); }
+  }
+#undef RQ_L
 }
 
 template <int W, int S>
@@ -643,16 +1251,18 @@ bool stream_supported(int nt, bool t3, int rl, bool norm) {
 
 void launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
                           int32_t* seg_tiles, int64_t cap, hipStream_t st) {
-  if (stream_shape() == 42) launch_shape<4, 2>(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
+  const int shape = stream_shape();
+  if (shape == 88) launch_pp_shape(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
+  else if (shape == 42) launch_shape<4, 2>(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
   else launch_shape<8, 3>(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
 }
 
 }  // namespace rqsid
 
 #ifdef RQSID_STAMPS
-extern "C" int rqsid_debug_stamps(unsigned long long* out4) {
-  if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_stamps), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
-  const unsigned long long z[4] = {0, 0, 0, 0};
+extern "C" int rqsid_debug_stamps(unsigned long long* out8) {
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stamps), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -43,6 +43,14 @@ def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000))):
     encmod.ops.assign = hook
     enc.encode(x)
     stream = os.environ.get("RQSID_SCREEN_VARIANT") == "5"
+    if stream and os.environ.get("RQSID_STREAM_SHAPE") == "88":  # ping-pong: per group {total, wait, compute, epilogue}
+        for lvl, v in enumerate(res):
+            for g in (0, 1):
+                tot, wt, cp, ep = v[4 * g:4 * g + 4]
+                f = lambda x: f"{100 * x / max(tot, 1):.1f}%"
+                print(f"L{lvl} group {g}: cycles {tot:.4g}  wait+barrier {f(wt)}  compute {f(cp)}  epilogue {f(ep)}  "
+                      f"issue/header {f(tot - wt - cp - ep)}", flush=True)
+        return
     for lvl, (tot, wt, ep, x, pro, *_) in enumerate(res):
         # x = cycles in the ring's DMA issue; pro = per-tile prologue (stream kernel: next-header steps)
         iss = x
