@@ -60,7 +60,7 @@ def parse():
 # kernels of each encode level's rqsid_assign call (per-tile screen + exact re-score; see encode.py)
 LEVEL_KERNELS = {0: ("assign_screen_kernel<4, 2, 0, false, false, true>", "assign_rescore_kernel<0, false>"),
                  1: ("assign_screen_kernel<4, 2, 1, true, true, true>", "assign_rescore_kernel<1, true>"),
-                 2: ("assign_screen_kernel<8, 2, 2, true, false, true>", "assign_rescore_kernel<2, true>")}
+                 2: ("assign_pp_kernel<8, 2, true, false>", "assign_rescore_kernel<2, true>")}
 
 
 def level_traffic(path, lvl):
@@ -262,7 +262,7 @@ def main():
     dom = max((k for k in kern if k.startswith("assign")), key=lambda k: kern[k]["ms"])
     dk = kern[dom]
     traffic = level_traffic(args.traffic_json, int(dom[-1])) if os.environ.get("RQSID_SCREEN_VARIANT", "0") == "0" else None
-    roof = {"kernel": dom + " (rqsid_assign: assign_screen_kernel + assign_rescore_kernel)", "bound": "hbm",
+    roof = {"kernel": dom + " (rqsid_assign: fp16 MFMA screen kernel + exact re-score kernel)", "bound": "hbm",
             "achieved": dk["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dk["hbm_frac"],
             "traffic": traffic, "traffic_unit": "bytes per launch",
             "traffic_source": (os.path.relpath(args.traffic_json, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "

@@ -894,8 +894,9 @@ void set_attrs(bool* ok) {
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) *ok = false;
 }
 
-// screen variant (tuning / A-B tests): 0 default (per-tile kernel); 2: multi-sweep list epilogue on
-// single-pass segments; 5: the persistent streamed kernel (assign_stream.hip) where it applies
+// screen variant (tuning / A-B tests): 0 default (per level: see rqsid_assign); 1: per-tile kernel
+// only; 2: per-tile kernel with the multi-sweep list epilogue on single-pass segments; 5: the
+// persistent streamed kernels (assign_stream.hip, RQSID_STREAM_SHAPE) where they apply
 int screen_variant() {  // read per call: tests switch it within one process
   const char* e = getenv("RQSID_SCREEN_VARIANT");
   return e ? atoi(e) : 0;
@@ -1037,12 +1038,18 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   // the persistent streamed kernel (assign_stream.hip): 512-d rows, single-pass segments, no local-id
   // remap, den_out present whenever it normalises a first-level residual
   const int nt = t3 || cand_count_max <= 128 ? 4 : 8;
-  const bool use_stream = screen_variant() == 5 && dim == 512 && cand_count_max <= 256 && !cand_lid &&
-                      (res_levels != 1 || !norm || den_out) && n_rows >= 64 * 256 &&
-                      (int64_t)n_segments + 1 <= n_rows && stream_supported(nt, t3, res_levels, norm);
+  const bool stream_ok = dim == 512 && cand_count_max <= 256 && !cand_lid && (res_levels != 1 || !norm || den_out) &&
+                         n_rows >= 64 * 256 && (int64_t)n_segments + 1 <= n_rows &&
+                         stream_supported(nt, t3, res_levels, norm);
+  // Default (variant 0): the ping-pong form for 1-term 256-candidate levels (measured L2 of the bench
+  // 7.58 vs 7.92 ms), the per-tile kernel elsewhere (L0 3.37 vs 3.99, L1 6.04 vs 6.54 ms).
+  // Variant 1 forces the per-tile kernel, variant 5 the stream forms (RQSID_STREAM_SHAPE).
+  const int variant = screen_variant();
+  const int shape = variant == 5 ? 0 : (variant == 0 && nt == 8 && !t3 ? 88 : -1);
+  const bool use_stream = stream_ok && shape >= 0;
   if (use_stream) {
     // the 256-row tile offsets live in the compact-list area until the compaction pass
-    launch_stream_screen(p, nt, t3, res_levels, norm, tile_seg, work_idx, n_rows, st);
+    launch_stream_screen(p, nt, t3, res_levels, norm, tile_seg, work_idx, n_rows, shape, st);
     if ((rc = check_launch("assign_stream"))) return rc;
     hipLaunchKernelGGL(sentinel_compact_kernel, dim3((unsigned)cdiv(n_rows, kCompactRows)), dim3(256), 0, st, out_global,
                        n_rows, p.work_count, work_idx);

@@ -457,8 +457,9 @@ __device__ __forceinline__ void row_frag(const float4 xa, const float4 xc, const
 
 // table-wide epilogue constants written by rqsid_prepare_centers into meta row k:
 // {2^-s, max |ec2|/|c|, max |ec1|/|c|, max |c|} (rounded up)
+// shape: 88 ping-pong 8-wave form, 83 / 42 streamed 8x3 / 4x2 forms, 0 = RQSID_STREAM_SHAPE (default 83)
 void launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
-                          int32_t* seg_tile256, int64_t cap, hipStream_t st);
+                          int32_t* seg_tile256, int64_t cap, int shape, hipStream_t st);
 bool stream_supported(int nt, bool t3, int rl, bool norm);
 
 }  // namespace rqsid

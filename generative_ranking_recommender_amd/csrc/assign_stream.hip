@@ -1250,8 +1250,8 @@ bool stream_supported(int nt, bool t3, int rl, bool norm) {
 }
 
 void launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
-                          int32_t* seg_tiles, int64_t cap, hipStream_t st) {
-  const int shape = stream_shape();
+                          int32_t* seg_tiles, int64_t cap, int shape, hipStream_t st) {
+  if (shape == 0) shape = stream_shape();
   if (shape == 88) launch_pp_shape(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
   else if (shape == 42) launch_shape<4, 2>(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
   else launch_shape<8, 3>(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);

@@ -332,24 +332,35 @@ def test_multigroup_weighted_encode_vs_oracle():
     assert (got == ref).all()
 
 
-def _with_variant(v, fn):
+def _with_env(env, fn):
+    """Run fn with the kernel-selection environment variables in env (read by librqsid per call)."""
     import os
-    old = os.environ.get("RQSID_SCREEN_VARIANT")
-    os.environ["RQSID_SCREEN_VARIANT"] = str(v)
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
     try:
         return fn()
     finally:
-        if old is None:
-            del os.environ["RQSID_SCREEN_VARIANT"]
-        else:
-            os.environ["RQSID_SCREEN_VARIANT"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
+PER_TILE = {"RQSID_SCREEN_VARIANT": 1}
+# the default dispatch (ping-pong form on 256-candidate levels) and every streamed form, forced
+STREAMED = {"default": {"RQSID_SCREEN_VARIANT": 0},
+            "s83": {"RQSID_SCREEN_VARIANT": 5, "RQSID_STREAM_SHAPE": 83},
+            "s42": {"RQSID_SCREEN_VARIANT": 5, "RQSID_STREAM_SHAPE": 42},
+            "pp88": {"RQSID_SCREEN_VARIANT": 5, "RQSID_STREAM_SHAPE": 88}}
+
+
+@pytest.mark.parametrize("form", list(STREAMED))
 @pytest.mark.parametrize("shape", ["small", "prod"])
 @pytest.mark.parametrize("sem_name", ["train", "simplified"])
-def test_stream_kernel_equals_tile_kernel(shape, sem_name):
-    """The persistent streamed screen (assign_stream.hip, RQSID_SCREEN_VARIANT=5) and the per-tile
-    screen (assign.hip) return the exact argmin both: identical IDs on every level, with
+def test_stream_kernel_equals_tile_kernel(shape, sem_name, form):
+    """The persistent streamed screens (assign_stream.hip: 8x3, 4x2 and the ping-pong form) and the
+    per-tile screen (assign.hip) return the exact argmin all: identical IDs on every level, with
     partial candidate lists (32 of a 128-wide tile), penalty-free match lists and both semantics;
     the streamed run is also checked row by row against the fp64 oracle on a sample."""
     sem = {"train": HIERARCHICAL_TRAIN, "simplified": SIMPLIFIED}[sem_name]
@@ -361,8 +372,8 @@ def test_stream_kernel_equals_tile_kernel(shape, sem_name):
     x = gpu(xn)
     enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], list(need),
                     match=torch.from_numpy(cb["match"]), semantics=sem, device=DEV)
-    a = _with_variant(5, lambda: enc.encode(x).cpu().numpy())
-    b = _with_variant(0, lambda: enc.encode(x).cpu().numpy())
+    a = _with_env(STREAMED[form], lambda: enc.encode(x).cpu().numpy())
+    b = _with_env(PER_TILE, lambda: enc.encode(x).cpu().numpy())
     assert (a == b).all(), f"{int((a != b).any(1).sum())} rows differ between the streamed and per-tile screens"
     sel = np.arange(0, 40000, 37)
     ref = O.encode(xn[sel], [cb["c0"], cb["c1"], cb["c2"]], list(need), cb["match"],
@@ -374,15 +385,16 @@ def test_stream_kernel_equals_tile_kernel(shape, sem_name):
     assert (a[sel] == ref).all()
 
 
+@pytest.mark.parametrize("form", ["default", "s83", "pp88"])
 @pytest.mark.parametrize("k", [100, 128, 200, 256])
-def test_stream_nearest_partial_tiles(k):
+def test_stream_nearest_partial_tiles(k, form):
     """Single-segment nearest with k < NT*32 candidates (padding lanes masked) on the streamed path."""
     rng = np.random.default_rng(k)
     c = rng.standard_normal((k, 512)).astype(np.float32)
     x = (c[rng.integers(0, k, 30000)] + 0.3 * rng.standard_normal((30000, 512))).astype(np.float32)
     pc = ops.prepare_centers(gpu(c))
-    got = _with_variant(5, lambda: ops.nearest(gpu(x), pc).cpu().numpy())
-    tile = _with_variant(0, lambda: ops.nearest(gpu(x), pc).cpu().numpy())
+    got = _with_env(STREAMED[form], lambda: ops.nearest(gpu(x), pc).cpu().numpy())
+    tile = _with_env(PER_TILE, lambda: ops.nearest(gpu(x), pc).cpu().numpy())
     assert (got == tile).all()
     sel = np.arange(0, 30000, 29)
     assert (got[sel] == exact_ids(x[sel], c)).all()
