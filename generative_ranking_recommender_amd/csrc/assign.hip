@@ -46,8 +46,10 @@ __global__ __launch_bounds__(256) void centers_absmax_kernel(const float* __rest
 // ---------------------------------------------------------------------------
 // centre preparation
 // ---------------------------------------------------------------------------
-// c16 = [hi | lo] tables: hi = fp16(c 2^s), lo = fp16((c 2^s - hi) 2^12) (the 3-term screen's second
-// term; scaled by 2^12 so it stays in the fp16 normal range).  meta[k] = {|c|^2, |c|,
+// c16 [k][dim/32][2][32]: per centre and 32-dim chunk, 32 hi = fp16(c 2^s) then 32 lo = fp16((c 2^s -
+// hi) 2^12) (the 3-term screen's second term; scaled by 2^12 so it stays in the fp16 normal range), so
+// one chunk's two terms are one 128-B piece (tools/probe/dma_probe2: gathered 128-B pieces stream 9-14 %
+// faster than 64-B ones).  meta[k] = {|c|^2, |c|,
 // |c - (hi + lo 2^-12) 2^-s|, |c - hi 2^-s|}; meta[k_total].x holds the absmax bits while this runs
 // (centers_absmax_kernel) and 2^-s afterwards (centers_scale_kernel).
 __global__ __launch_bounds__(256) void prepare_centers_kernel(const float* __restrict__ c, int64_t k, int dim,
@@ -64,8 +66,9 @@ __global__ __launch_bounds__(256) void prepare_centers_kernel(const float* __res
     const _Float16 hv = to_f16(vs);
     const float r1 = vs - (float)hv;  // exact (or vs itself when hv was flushed)
     const _Float16 lv = to_f16(r1 * 4096.0f);
-    c16[row * dim + i] = hv;
-    c16[(k + row) * dim + i] = lv;
+    const int64_t o = row * 2 * dim + (i >> 5) * 64 + (i & 31);
+    c16[o] = hv;
+    c16[o + 32] = lv;
     const double e1 = (double)v - ldexp((double)(float)hv, -sx);  // exact residuals of what the MFMA sees
     const double e2 = e1 - ldexp((double)(float)lv, -sx - 12);
     s += (double)v * (double)v;
@@ -243,27 +246,21 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
   uint32_t pbits[ONE ? NT / 2 : 1];  // ONE: pass bits, word w = tiles 2w, 2w+1, MSB first
   for (int pass = 0; pass < npass; ++pass) {
     const int pbase = pass * NT * 32;
-    // centre DMA sources: instruction j covers candidates (wave*NT/2 + j)*16 + lane/4, slot lane%4
-    const _Float16* csrc[NT / 2];
-    const _Float16* clo[T3 ? NT / 2 : 1];
+    // centre DMA sources (c16 row = 2 dim halves, chunk c at 64 c).  1 term: instruction j covers the
+    // hi halves of candidates (wave*NT/2 + j)*16 + lane/4 (64 B each, slot lane%4 of the image row
+    // k*64 + (slot ^ ((k>>2)&3))*16); T3: instruction j covers the hi+lo pieces of candidates
+    // (wave*NT + j)*8 + lane/8 (128 B each, image row k*128 + (slot ^ ((k>>1)&7))*16: hi slots 0-3, lo 4-7)
+    constexpr int kCOps = T3 ? NT : NT / 2;
+    const _Float16* csrc[kCOps];
 #pragma unroll
-    for (int j = 0; j < NT / 2; ++j) {
-      const int il = (wave * (NT / 2) + j) * 16 + (lane >> 2);
+    for (int j = 0; j < kCOps; ++j) {
+      const int il = T3 ? (wave * NT + j) * 8 + (lane >> 3) : (wave * (NT / 2) + j) * 16 + (lane >> 2);
       const int kl = pbase + il < cnt ? pbase + il : cnt - 1;
       const int cg = cand_global(p, cbase, kl);
-      const int slot = (lane & 3) ^ ((il >> 2) & 3);
-#ifdef RQSID_AB_CMAJOR  // timing probe: chunk-major centre layout [dim/32][k][32] (wrong data)
-      csrc[j] = reinterpret_cast<const _Float16*>(p.c16) + (int64_t)cg * kChunk + slot * 8;
-#else
-      csrc[j] = reinterpret_cast<const _Float16*>(p.c16) + (int64_t)cg * dim + slot * 8;
-#endif
-      if (T3) clo[j] = csrc[j] + (int64_t)p.n_centers * dim;
+      const int slot = T3 ? (lane & 7) ^ ((il >> 1) & 7) : (lane & 3) ^ ((il >> 2) & 3);
+      csrc[j] = reinterpret_cast<const _Float16*>(p.c16) + (int64_t)cg * 2 * dim + slot * 8;
     }
-#ifdef RQSID_AB_CMAJOR
-    const int64_t kCStride = (int64_t)p.n_centers * kChunk;
-#else
-    constexpr int kCStride = kChunk;
-#endif
+    constexpr int kCStride = 2 * kChunk;
     // DMA op i of chunk c (x rows 0..3, hi centres, lo centres) into stage c % S
     auto issue_op = [&](int c, int i, bool relaxed) {
       const uint32_t sb = lds0 + (uint32_t)((c % S) * L::kStage);
@@ -272,10 +269,9 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
         const uint32_t dst = __builtin_amdgcn_readfirstlane(sb + wave * kXWaveBytes + i * 1024);
         if (relaxed) dma16_nt_r(src, dst); else dma16_nt(src, dst);
       } else {
-        const int j = (i - 4) % (NT / 2), lo = (i - 4) / (NT / 2);
-        const void* src = (lo ? clo[T3 ? j : 0] : csrc[j]) + c * kCStride;
-        const uint32_t dst =
-            __builtin_amdgcn_readfirstlane(sb + kXStage + lo * L::kCHalf + (wave * (NT / 2) + j) * 1024);
+        const int j = i - 4;
+        const void* src = csrc[j] + c * kCStride;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(sb + kXStage + (wave * kCOps + j) * 1024);
         if (relaxed) dma16_r(src, dst); else dma16(src, dst);
       }
     };
@@ -321,9 +317,8 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
       lds_meta[tid] = make_float4(live ? m.x : INFINITY, m.y, T3 ? m.z : m.w, m.w);
     }
 #pragma unroll
-    for (int j = 0; j < NT / 2; ++j) {
+    for (int j = 0; j < kCOps; ++j) {
       asm volatile("" : "+v"(csrc[j]));
-      if (T3) asm volatile("" : "+v"(clo[j]));
     }
     __syncthreads();
 
@@ -344,7 +339,9 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
 #endif
       constexpr int NG = 2 * NT;
       const unsigned char* xb = smem + (c % S) * L::kStage + wave * kXWaveBytes + r * 128;
-      const unsigned char* cbp = smem + (c % S) * L::kStage + kXStage + r * 64;
+      // centre image row of candidate t*32 + r: 64 B (1 term) or 128 B (T3: hi slots 0-3, lo 4-7)
+      const unsigned char* cbp = smem + (c % S) * L::kStage + kXStage + r * (T3 ? 128 : 64);
+      const int tsw = (r >> 1) & 7;  // T3 image swizzle (the x image's)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int q0 = 4 * ks + 2 * h;
@@ -354,10 +351,11 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
         f16x8 bf, bl = {};
         if (pass == 0) row_frag<RL, NORM, T3, true>(xa, xc, lds_ca, lds_cb, d0, inv1, bf, bl, rs);
         else row_frag<RL, NORM, T3, false>(xa, xc, lds_ca, lds_cb, d0, inv1, bf, bl, rs);
-        const int qa = (2 * ks + h) ^ csw;
+        const int qa = T3 ? (2 * ks + h) ^ tsw : (2 * ks + h) ^ csw;
+        const int ql = (4 + 2 * ks + h) ^ tsw;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          const f16x8 af = *reinterpret_cast<const f16x8*>(cbp + t * 32 * 64 + (qa << 4));
+          const f16x8 af = *reinterpret_cast<const f16x8*>(cbp + t * 32 * (T3 ? 128 : 64) + (qa << 4));
 #if RQSID_AB_MODE >= 2
           acc[t][0] += (float)bf[0] + (float)af[0];
           if (false) {
@@ -365,7 +363,7 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc[t], 0, 0, 0);
           if (T3) {
 #endif
-            const f16x8 al = *reinterpret_cast<const f16x8*>(cbp + L::kCHalf + t * 32 * 64 + (qa << 4));
+            const f16x8 al = *reinterpret_cast<const f16x8*>(cbp + t * 32 * 128 + (ql << 4));
             accl[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bl, accl[t], 0, 0, 0);
             accl[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bf, accl[t], 0, 0, 0);
           }

@@ -44,7 +44,7 @@ struct AssignParams {
   const int32_t* seg_row_off;
   const int32_t* seg_tile_off;
   const float* centers;
-  const uint16_t* c16;   // fp16 bits [2][k][dim]: hi, lo tables (rqsid_prepare_centers)
+  const uint16_t* c16;   // fp16 bits [k][dim/32][2][32]: per chunk hi then lo terms (rqsid_prepare_centers)
   const float* c_meta;   // [k+1] float4: per centre |c|^2, |c|, |c - (hi + lo 2^-12) 2^-s|, |c - hi 2^-s|; row k: 2^-s
   int32_t n_centers;
   const int32_t* cand_base;

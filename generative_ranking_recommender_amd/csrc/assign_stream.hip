@@ -143,7 +143,6 @@ __global__ __launch_bounds__(W * 64, 2) void assign_stream_kernel(AssignParams p
   const float tgz = __uint_as_float(uni(__float_as_uint(trow[1])));
   const float tgw = __uint_as_float(uni(__float_as_uint(trow[2])));
   const float tgy = __uint_as_float(uni(__float_as_uint(trow[3])));
-  const int64_t lo_off = (int64_t)p.n_centers * kSDim;  // T3: the lo table follows the hi table
   int* const dummy = p.work_count + 16;                 // sink of the fixed-count stores
 
   // ---- header pipeline pieces -------------------------------------------------------------
@@ -197,12 +196,12 @@ __global__ __launch_bounds__(W * 64, 2) void assign_stream_kernel(AssignParams p
       n.xi[i] = (uint32_t)row_of(lr) * 128u + (uint32_t)sl;
     }
     // centre image: candidate k at k*64 B, slot q stored at q ^ ((k>>2)&3); instruction j of wave w
-    // moves candidates (w*NT/4 + j)*16 + lane/4, physical slot lane%4
+    // moves candidates (w*NT/4 + j)*16 + lane/4, physical slot lane%4 (sources: 2-KiB c16 rows)
 #pragma unroll
     for (int j = 0; j < kCI; ++j) {
       const int k = (wave * kCI + j) * 16 + (lane >> 2);
       const int sl = (lane & 3) ^ ((k >> 2) & 3);
-      n.ci[j] = (uint32_t)cand_of(H, par, k) * 64u + (uint32_t)sl;
+      n.ci[j] = (uint32_t)cand_of(H, par, k) * 128u + (uint32_t)sl;
     }
   };
   // level 2: |c|^2 and |c| of the candidates (SoA, gathered from meta), den_in of the rows (RL2 NORM)
@@ -230,11 +229,11 @@ __global__ __launch_bounds__(W * 64, 2) void assign_stream_kernel(AssignParams p
     const char* xb = xbase + c * (kSC * 4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) dma16_nt(addr(xb, n.xi[i]), uni(sb + wave * 4096 + i * 1024));
-    const char* cb = cbase16 + c * (kSC * 2);
+    const char* cb = cbase16 + c * (kSC * 4);  // c16 row: per chunk 64 B hi then 64 B lo
 #pragma unroll
     for (int j = 0; j < kCI; ++j) dma16(addr(cb, n.ci[j]), uni(sb + kSX + (wave * kCI + j) * 1024));
     if (T3) {
-      const char* cl = cb + lo_off * 2;
+      const char* cl = cb + kSC * 2;
 #pragma unroll
       for (int j = 0; j < kCI; ++j)
         dma16(addr(cl, n.ci[j]), uni(sb + kSX + L::kCen + (wave * kCI + j) * 1024));
@@ -650,7 +649,6 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
   const float tgz = __uint_as_float(uni(__float_as_uint(trow[1])));
   const float tgw = __uint_as_float(uni(__float_as_uint(trow[2])));
   const float tgy = __uint_as_float(uni(__float_as_uint(trow[3])));
-  const int64_t lo_off = (int64_t)p.n_centers * kSDim;  // T3: the lo table follows the hi table
   int* const dummy = p.work_count + 16;                 // sink of the fixed-count stores
 
   // ---- header pipeline pieces -------------------------------------------------------------
@@ -704,12 +702,12 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
       n.xi[i] = (uint32_t)row_of(lr) * 128u + (uint32_t)sl;
     }
     // centre image: candidate k at k*64 B, slot q stored at q ^ ((k>>2)&3); instruction j of wave w
-    // moves candidates (w*NT/4 + j)*16 + lane/4, physical slot lane%4
+    // moves candidates (w*NT/4 + j)*16 + lane/4, physical slot lane%4 (sources: 2-KiB c16 rows)
 #pragma unroll
     for (int j = 0; j < kCI; ++j) {
       const int k = (gw * kCI + j) * 16 + (lane >> 2);
       const int sl = (lane & 3) ^ ((k >> 2) & 3);
-      n.ci[j] = (uint32_t)cand_of(H, par, k) * 64u + (uint32_t)sl;
+      n.ci[j] = (uint32_t)cand_of(H, par, k) * 128u + (uint32_t)sl;
     }
   };
   // level 2: |c|^2 and |c| of the candidates (SoA, gathered from meta), den_in of the rows (RL2 NORM)
@@ -733,11 +731,11 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
   int qb = 0;  // row stage of this tile's chunk 0 (16 % 3 != 0: walks on across tiles)
   auto issue_c = [&](const Next& n, int j) __attribute__((always_inline)) {  // group 1: chunk j's centres
     const uint32_t sc = lds0 + L::kC + (j & 1) * L::kCStage;
-    const char* cb = cbase16 + (j & 15) * (kSC * 2);
+    const char* cb = cbase16 + (j & 15) * (kSC * 4);  // c16 row: per chunk 64 B hi then 64 B lo
 #pragma unroll
     for (int q = 0; q < kCI; ++q) dma16(addr(cb, n.ci[q]), uni(sc + (gw * kCI + q) * 1024));
     if (T3) {
-      const char* cl = cb + lo_off * 2;
+      const char* cl = cb + kSC * 2;
 #pragma unroll
       for (int q = 0; q < kCI; ++q) dma16(addr(cl, n.ci[q]), uni(sc + L::kCen + (gw * kCI + q) * 1024));
     }

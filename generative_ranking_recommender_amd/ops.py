@@ -50,7 +50,7 @@ def centroid_tile_rows() -> int:
 class PreparedCenters:
     """Centres + the derived data rqsid_assign reads (fp16 copy and screening-bound norms)."""
     centers: torch.Tensor      # f32 [K, D]
-    c16: torch.Tensor          # int16 [2, K, D]: hi, lo fp16 terms of c 2^s (IEEE half bits)
+    c16: torch.Tensor          # int16 [K, D/32, 2, 32]: per 32-dim chunk the hi then lo fp16 terms of c 2^s
     meta: torch.Tensor         # f32 [K+1, 4]: |c|^2, |c|, |2-term residual|, |1-term residual|; row K: 2^-s
 
     @property
@@ -66,7 +66,7 @@ def prepare_centers(c: torch.Tensor) -> PreparedCenters:
     c = c.float().contiguous()
     _require_device(c)
     k, d = c.shape
-    c16 = torch.empty((2, k, d), dtype=torch.int16, device=c.device)
+    c16 = torch.empty((k, d // 32, 2, 32), dtype=torch.int16, device=c.device)
     meta = torch.empty((k + 1, 4), dtype=torch.float32, device=c.device)
     _lib.check(lib().rqsid_prepare_centers(_ptr(c), k, d, _ptr(c16), _ptr(meta), _stream()),
                "rqsid_prepare_centers")

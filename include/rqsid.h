@@ -41,7 +41,8 @@ const char* rqsid_last_error(void);
 /* Centre preparation for rqsid_assign.  The table is scaled by a power of two 2^s (largest element
  * just below 2^14) and split into two fp16 terms: hi = fp16(c 2^s) and lo = fp16((c 2^s - hi) 2^12),
  * scaled values outside the fp16 normal range stored as 0 (the MFMA must never see a subnormal).
- * c16 [2][k][dim] (IEEE half bits: the hi table, then the lo table); c_meta [k+1][4]: row j <  k =
+ * c16 [k][dim/32][2][32] (IEEE half bits: per centre and 32-dim chunk, 32 hi terms then 32 lo terms,
+ * one 128-B piece); c_meta [k+1][4]: row j <  k =
  * {|c|^2, |c|, |c - (hi + lo 2^-12) 2^-s|, |c - hi 2^-s|} (fp64-accumulated, feeding the screening
  * error bound), row k = {2^-s, max_j |c - (hi + lo 2^-12) 2^-s| / |c|, max_j |c - hi 2^-s| / |c|,
  * max_j |c|} (rounded up; the single-pass screens collapse their per-candidate bound onto |c|).  Replaces the per-call centre side of torch.cdist's

@@ -97,7 +97,7 @@ def test_nearest_extreme_scales(xs, cs, terms):
 
 
 def test_prepare_centers_table_scale():
-    """c16 = [hi | lo]: hi = fp16(c 2^s) with the largest |hi| in [2^13, 2^14), lo = fp16((c 2^s - hi)
+    """c16 [k][dim/32][hi|lo][32]: hi = fp16(c 2^s) with the largest |hi| in [2^13, 2^14), lo = fp16((c 2^s - hi)
     2^12), no subnormals; meta rows {|c|^2, |c|, |2-term residual|, |1-term residual|}, row k = 2^-s."""
     rng = np.random.default_rng(5)
     c = (rng.standard_normal((300, 256)) * 3e-3).astype(np.float32)
@@ -107,7 +107,8 @@ def test_prepare_centers_table_scale():
     scale = float(meta[300, 0])
     assert np.log2(scale) == np.round(np.log2(scale))
     hl = pc.c16.cpu().numpy().view(np.float16).astype(np.float64)
-    hi, lo = hl[0], hl[1]
+    assert hl.shape == (300, 256 // 32, 2, 32)
+    hi, lo = hl[:, :, 0, :].reshape(300, 256), hl[:, :, 1, :].reshape(300, 256)
     assert 2.0 ** 13 <= np.abs(hi).max() < 2.0 ** 14
     for t in (hi, lo):
         assert ((np.abs(t) >= 2.0 ** -14) | (t == 0)).all()

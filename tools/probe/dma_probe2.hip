@@ -25,7 +25,7 @@ template <int N> __device__ __forceinline__ void waitb() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"i"(N) : "memory");
 }
 
-template <int W, int S, int NC, bool NTX>
+template <int W, int S, int NC, bool NTX, int CP>
 __global__ __launch_bounds__(W * 64) void probe(const char* __restrict__ x, const int* __restrict__ perm,
                                                 const char* __restrict__ ctab, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -50,8 +50,13 @@ __global__ __launch_bounds__(W * 64) void probe(const char* __restrict__ x, cons
     }
 #pragma unroll
     for (int j = 0; j < PC; ++j) {
-      const int cand = ((t * 977) + (wave * PC + j) * 16 + lane / 4) % 2560;
-      co[j] = ctab + (size_t)cand * 1024 + (lane % 4) * 16;
+      if (CP == 64) {  // 16 candidates x 64 B (32 fp16 dims) per op
+        const int cand = ((t * 977) + (wave * PC + j) * 16 + lane / 4) % 2560;
+        co[j] = ctab + (size_t)cand * 1024 + (lane % 4) * 16;
+      } else {  // 8 candidates x 128 B (64 dims) per op; a chunk pair covers every candidate
+        const int cand = ((t * 977) + (wave * PC + j) * 8 + lane / 8) % 2560;
+        co[j] = ctab + (size_t)cand * 1024 + (lane % 8) * 16;
+      }
     }
   };
   auto issue = [&](const char** xo, const char** co, int c, int st) {
@@ -59,7 +64,10 @@ __global__ __launch_bounds__(W * 64) void probe(const char* __restrict__ x, cons
 #pragma unroll
     for (int i = 0; i < PX; ++i) dma16<NTX>(xo[i] + c * 128, __builtin_amdgcn_readfirstlane(sb + (wave * PX + i) * 1024));
 #pragma unroll
-    for (int j = 0; j < PC; ++j) dma16(co[j] + c * 64, __builtin_amdgcn_readfirstlane(sb + XS + (wave * PC + j) * 1024));
+    for (int j = 0; j < PC; ++j) {
+      const size_t off = CP == 64 ? (size_t)c * 64 : (size_t)(c >> 1) * 128 + (size_t)(c & 1) * (NC / 2) * 1024;
+      dma16(co[j] + off, __builtin_amdgcn_readfirstlane(sb + XS + (wave * PC + j) * 1024));
+    }
   };
   const char* xc[PX]; const char* cc[PC > 0 ? PC : 1];
   const char* xn[PX]; const char* cn[PC > 0 ? PC : 1];
@@ -86,23 +94,23 @@ __global__ __launch_bounds__(W * 64) void probe(const char* __restrict__ x, cons
   }
 }
 
-template <int W, int S, int NC, bool NTX>
+template <int W, int S, int NC, bool NTX, int CP>
 void run(const char* x, const int* perm, const char* ctab, int n, int ncu, int bpc) {
   const int R = 32 * W, ntiles = n / R;
   const int lds = S * (R * 128 + NC * 64);
   if (lds * bpc > 160 * 1024) { printf("W=%d S=%d NC=%d bpc=%d: LDS %d too big\n", (int)NTX, W, S, NC, bpc, lds); return; }
   const int alloc = std::max(lds, 160 * 1024 / bpc - 1024);
-  hipFuncSetAttribute((const void*)probe<W, S, NC, NTX>, hipFuncAttributeMaxDynamicSharedMemorySize, alloc);
+  hipFuncSetAttribute((const void*)probe<W, S, NC, NTX, CP>, hipFuncAttributeMaxDynamicSharedMemorySize, alloc);
   const int grid = std::min(ntiles, ncu * bpc);
   hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
-  hipLaunchKernelGGL((probe<W, S, NC, NTX>), dim3(grid), dim3(W * 64), alloc, 0, x, perm, ctab, ntiles);
+  hipLaunchKernelGGL((probe<W, S, NC, NTX, CP>), dim3(grid), dim3(W * 64), alloc, 0, x, perm, ctab, ntiles);
   hipEventRecord(a);
-  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((probe<W, S, NC, NTX>), dim3(grid), dim3(W * 64), alloc, 0, x, perm, ctab, ntiles);
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((probe<W, S, NC, NTX, CP>), dim3(grid), dim3(W * 64), alloc, 0, x, perm, ctab, ntiles);
   hipEventRecord(b); hipEventSynchronize(b);
   float ms; hipEventElapsedTime(&ms, a, b); ms /= 3;
   if (hipGetLastError() != hipSuccess) { printf("error\n"); return; }
   const double bytes = (double)ntiles * R * 2048;
-  printf("nt=%d waves=%d S=%d cands=%d blocks/CU=%d x-inflight/CU=%3d KB lds=%3d KB  %.3f ms  %.0f GB/s (x)\n", (int)NTX, W, S, NC, bpc,
+  printf("cp=%d nt=%d waves=%d S=%d cands=%d blocks/CU=%d x-inflight/CU=%3d KB lds=%3d KB  %.3f ms  %.0f GB/s (x)\n", CP, (int)NTX, W, S, NC, bpc,
          (S - 1) * R * 128 * bpc / 1024, lds / 1024, ms, bytes / ms / 1e6);
   fflush(stdout);
 }
@@ -117,8 +125,8 @@ int main() {
   hipMemcpy(perm, p.data(), (size_t)n * 4, hipMemcpyHostToDevice);
   hipDeviceProp_t prop; hipGetDeviceProperties(&prop, 0);
   const int ncu = prop.multiProcessorCount;
-#define R(W, S, NC, B, T) run<W, S, NC, T>(x, perm, ctab, n, ncu, B);
-  R(4, 2, 256, 2, false) R(4, 2, 256, 2, true) R(8, 3, 256, 1, false) R(8, 3, 256, 1, true)
-  R(8, 3, 128, 1, true) R(4, 2, 128, 3, true) R(4, 3, 128, 2, true) R(8, 3, 0, 1, true) R(4, 2, 0, 3, true)
+#define R(W, S, NC, B, T, CP) run<W, S, NC, T, CP>(x, perm, ctab, n, ncu, B);
+  R(4, 2, 256, 2, true, 64) R(4, 2, 256, 2, true, 128) R(8, 3, 256, 1, true, 64) R(8, 3, 256, 1, true, 128)
+  R(4, 2, 128, 3, true, 64) R(4, 2, 128, 3, true, 128) R(8, 3, 0, 1, true, 64) R(4, 2, 0, 3, true, 64)
   return 0;
 }
