@@ -19,6 +19,11 @@ SRCS = [PKG / "csrc" / "rqsid.hip", PKG / "csrc" / "assign.hip", PKG / "csrc" / 
         PKG / "csrc" / "auction.hip"]
 DEPS = SRCS + [PKG / "csrc" / "internal.h", PKG / "csrc" / "assign_common.h"]
 HEADER = REPO / "include" / "rqsid.h"
+# host-only I/O library (CSV reader): plain g++, no GPU code
+IO_LIB_PATH = PKG / "librqsid_io.so"
+IO_SRCS = [PKG / "csrc" / "csv_loader.cpp"]
+IO_HEADER = REPO / "include" / "rqsid_io.h"
+IO_FLAGS = ["-O3", "-std=c++17", "-Wall", "-shared", "-fPIC", "-pthread"]
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-shared", "-fPIC"]
 
@@ -53,7 +58,20 @@ SIGNATURES = {
     "rqsid_mfma_probe": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 
+IO_SIGNATURES = {
+    "rqsid_csv_open": (c_i32, [c_char_p, c_i32, c_i64, c_i32, c_vp]),
+    "rqsid_csv_rows": (c_i64, [c_vp]),
+    "rqsid_csv_id_bytes": (c_i64, [c_vp]),
+    "rqsid_csv_nonnumeric": (c_i64, [c_vp]),
+    "rqsid_csv_records": (c_i64, [c_vp]),
+    "rqsid_csv_copy": (c_i32, [c_vp, c_vp, c_vp, c_vp]),
+    "rqsid_csv_copy_f16": (c_i32, [c_vp, c_vp]),
+    "rqsid_csv_close": (None, [c_vp]),
+    "rqsid_io_last_error": (c_char_p, []),
+}
+
 _lib = None
+_io_lib = None
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
@@ -68,6 +86,37 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
+
+
+def build_io(force: bool = False, verbose: bool = False) -> Path:
+    """Compile the host I/O library (g++)."""
+    if (IO_LIB_PATH.exists() and not force
+            and IO_LIB_PATH.stat().st_mtime >= max(f.stat().st_mtime for f in IO_SRCS + [IO_HEADER])):
+        return IO_LIB_PATH
+    tmp = IO_LIB_PATH.with_suffix(".so.tmp")
+    cmd = [os.environ.get("CXX", "g++"), *IO_FLAGS, "-o", str(tmp), *map(str, IO_SRCS)]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, IO_LIB_PATH)
+    return IO_LIB_PATH
+
+
+def load_io():
+    """Load librqsid_io.so and bind every symbol of include/rqsid_io.h (raises if absent)."""
+    global _io_lib
+    if _io_lib is not None:
+        return _io_lib
+    if not IO_LIB_PATH.exists():
+        raise RuntimeError(f"host I/O library {IO_LIB_PATH} is missing: run "
+                           "`python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(str(IO_LIB_PATH))
+    for name, (res, args) in IO_SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _io_lib = lib
+    return lib
 
 
 def load():

@@ -4,7 +4,8 @@
   src/common/train_word2vec.py:69-73, read with the rules of simplified_semantic_id_generator.py:38-76
   and train_semantic_ids.py:72-131 (rows with < 2 fields skipped, non-numeric rows skipped, rows of
   another dimension skipped, ValueError when nothing is left, values rounded to fp16 when any
-  ``layer_clusters`` entry exceeds 512).
+  ``layer_clusters`` entry exceeds 512).  Native multi-threaded reader (``csrc/csv_loader.cpp``,
+  include/rqsid_io.h); the Python-csv restatement it is checked against is ``oracle/csv_oracle.py``.
 * ``write_semantic_ids`` — one ``json.dumps({"song_id": ..., "semantic_ids": [...]})`` line per song
   (simplified :368-385, train_semantic_ids.py:239-264), byte-identical to the reference.
 * ``semantic_id_statistics`` / ``training_config`` — the side files training_statistics.json and
@@ -13,6 +14,7 @@
 from __future__ import annotations
 
 import csv
+import ctypes
 import json
 import logging
 import os
@@ -20,37 +22,53 @@ from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
 
+from . import _lib
+
 logger = logging.getLogger(__name__)
 
 
 def load_song_vectors(path: str, embedding_dim: int, layer_clusters: Sequence[int] = (),
-                      limit: int | None = None) -> Tuple[List[str], np.ndarray]:
+                      limit: int | None = None, n_threads: int = 0) -> Tuple[List[str], np.ndarray]:
     """Returns (song_ids, vectors): float16 when any layer_clusters > 512 (the reference's
-    ``.half()``), float32 otherwise."""
-    if not os.path.isfile(path):
-        raise FileNotFoundError(f"The specified data file was not found: {path}")
-    song_ids: List[str] = []
-    rows: List[np.ndarray] = []
-    with open(path, "r", encoding="utf-8") as f:
-        for i, row in enumerate(csv.reader(f)):
-            if limit and i >= limit:
-                break
-            if len(row) < 2:
-                continue
-            try:
-                embed = np.array(row[1:], dtype=np.float32)
-            except ValueError:
-                logger.warning("Skipping row for song_id %s due to non-numeric vector data.", row[0])
-                continue
-            if embed.shape[0] == embedding_dim:
-                song_ids.append(row[0])
-                rows.append(embed)
-    if not song_ids:
-        raise ValueError("No valid data with the correct embedding dimension found in the CSV file.")
-    x = np.vstack(rows)
-    if any(n > 512 for n in layer_clusters):
-        x = x.astype(np.float16)
+    ``.half()``), float32 otherwise.  Parsed by the native multi-threaded reader
+    (``librqsid_io.so``, include/rqsid_io.h); raises if the library is missing."""
+    lib = _lib.load_io()
+    h = ctypes.c_void_p()
+    rc = lib.rqsid_csv_open(os.fsencode(path), int(embedding_dim), int(limit or 0), int(n_threads),
+                            ctypes.byref(h))
+    msg = lib.rqsid_io_last_error().decode(errors="replace")
+    if rc == 1:
+        raise FileNotFoundError(msg)
+    if rc == -1:
+        raise ValueError(msg)
+    if rc not in (0, 2):
+        raise RuntimeError(f"rqsid_csv_open failed ({rc}): {msg}")
+    try:
+        bad = lib.rqsid_csv_nonnumeric(h)
+        if bad:
+            logger.warning("Skipped %d rows due to non-numeric vector data.", bad)
+        if rc == 2:
+            raise ValueError(msg)
+        n, nbytes = lib.rqsid_csv_rows(h), lib.rqsid_csv_id_bytes(h)
+        half = any(k > 512 for k in layer_clusters)
+        x = np.empty((n, embedding_dim), dtype=np.float16 if half else np.float32)
+        ids = np.empty(max(nbytes, 1), dtype=np.uint8)
+        off = np.empty(n + 1, dtype=np.int64)
+        vp = ctypes.c_void_p
+        _check_io(lib, lib.rqsid_csv_copy(h, None if half else vp(x.ctypes.data), vp(ids.ctypes.data),
+                                          vp(off.ctypes.data)))
+        if half:
+            _check_io(lib, lib.rqsid_csv_copy_f16(h, vp(x.ctypes.data)))
+    finally:
+        lib.rqsid_csv_close(h)
+    blob = ids.tobytes()
+    song_ids = [blob[off[i]:off[i + 1]].decode("utf-8") for i in range(n)]
     return song_ids, x
+
+
+def _check_io(lib, rc: int) -> None:
+    if rc != 0:
+        raise RuntimeError(f"librqsid_io failed ({rc}): {lib.rqsid_io_last_error().decode(errors='replace')}")
 
 
 def write_song_vectors(path: str, song_ids: Sequence[str], vectors: np.ndarray) -> None:
