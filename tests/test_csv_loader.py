@@ -155,3 +155,22 @@ def test_errors(tmp_path):
     e.write_text("")
     with pytest.raises(ValueError):
         rq_io.load_song_vectors(str(e), 2)
+
+
+def test_integration_md_csv_stub_runs(tmp_path, monkeypatch):
+    """The ctypes stub INTEGRATION.md shows for the reference's loaders returns what the reference's
+    reader returns (ids, and the fp16 tensor for PROD layer_clusters)."""
+    import torch
+    text = (_lib.REPO / "INTEGRATION.md").read_text()
+    code = re.search(r"```python\n(# semantic_id_generator/_rqsid_io.py.*?)```", text, re.S).group(1)
+    monkeypatch.setenv("RQSID_IO_LIB", str(_lib.IO_LIB_PATH))
+    ns = {}
+    exec(compile(code, "INTEGRATION.md", "exec"), ns)
+    p = tmp_path / "s.csv"
+    x = np.random.default_rng(3).standard_normal((50, 8)).astype(np.float32)
+    rq_io.write_song_vectors(str(p), [f"id{i}" for i in range(50)], x)
+    ids, t = ns["load_data"](str(p), 8, [128, 1280, 1280])
+    rids, rx, _ = csv_oracle.load_song_vectors(str(p), 8, [128, 1280, 1280])
+    assert ids == rids and t.dtype == torch.float16 and np.array_equal(t.numpy(), rx)
+    with pytest.raises(FileNotFoundError):
+        ns["load_data"](str(tmp_path / "nope.csv"), 8, [128])
