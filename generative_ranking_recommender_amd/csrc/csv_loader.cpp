@@ -43,6 +43,81 @@ struct Part {
 inline bool is_eol(char c) { return c == '\n' || c == '\r'; }
 inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\f' || c == '\v'; }
 
+// Correctly rounded decimal -> double for the common case, without strtod: s..e is a validated literal
+// (sign, digits, '.', exponent; no underscores).  With at most 19 significant digits the literal is
+// w 10^q exactly (w < 2^64).  |q| <= 22 and w <= 2^53: one IEEE operation on exact operands (Clinger).
+// |q| <= 27: x87 extended arithmetic (10^27 = 5^27 2^27 is exact in a 64-bit significand) gives w 10^q
+// within one unit of the 64-bit significand; rounding that to double is correct unless its 11 extra
+// bits sit within one unit of the halfway pattern 0x400.  Anything else returns false (caller: strtod).
+bool fast_decimal(const char* s, const char* e, double* out) {
+  static const double p10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                 1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  bool neg = false;
+  if (s < e && (*s == '-' || *s == '+')) neg = *s++ == '-';
+  uint64_t w = 0;
+  int nd = 0, q = 0;
+  for (; s < e && *s >= '0' && *s <= '9'; ++s) {
+    if (nd || *s != '0') {
+      if (nd == 19) return false;
+      w = w * 10 + (uint64_t)(*s - '0');
+      ++nd;
+    }
+  }
+  if (s < e && *s == '.') {
+    for (++s; s < e && *s >= '0' && *s <= '9'; ++s) {
+      if (nd || *s != '0') {
+        if (nd == 19) return false;
+        w = w * 10 + (uint64_t)(*s - '0');
+        ++nd;
+      }
+      --q;
+    }
+  }
+  if (s < e && (*s == 'e' || *s == 'E')) {
+    ++s;
+    bool eneg = false;
+    if (s < e && (*s == '-' || *s == '+')) eneg = *s++ == '-';
+    int x = 0;
+    for (; s < e && *s >= '0' && *s <= '9'; ++s) {
+      if (x > 10000) return false;
+      x = x * 10 + (*s - '0');
+    }
+    q += eneg ? -x : x;
+  }
+  if (s != e) return false;
+  if (w == 0) {
+    *out = neg ? -0.0 : 0.0;
+    return true;
+  }
+  if (q < -27 || q > 27) return false;
+  double d;
+  if (w <= (1ull << 53) && q >= -22 && q <= 22) {
+    d = (double)w;
+    d = q < 0 ? d / p10[-q] : d * p10[q];
+  } else {
+    static const struct P10L {  // 10^0 .. 10^27, exact in the x87 64-bit significand
+      long double v[28];
+      P10L() {
+        v[0] = 1.0L;
+        for (int i = 1; i < 28; ++i) v[i] = v[i - 1] * 10.0L;
+      }
+    } lp;
+    const long double r = q < 0 ? (long double)w / lp.v[-q] : (long double)w * lp.v[q];
+    // x87 extended layout: explicit 64-bit significand, then sign and 15-bit exponent (bias 16383)
+    uint64_t bits;
+    uint16_t se;
+    memcpy(&bits, &r, 8);
+    memcpy(&se, reinterpret_cast<const char*>(&r) + 8, 2);
+    const int ex = (int)(se & 0x7fff) - 16383;
+    if (ex < -1020 || ex > 1022) return false;  // keep clear of double subnormals and overflow
+    const uint32_t low = (uint32_t)(bits & 0x7ffu);
+    if (low >= 0x3ffu && low <= 0x401u) return false;
+    d = (double)r;
+  }
+  *out = neg ? -d : d;
+  return true;
+}
+
 // Python float(str) for ASCII text: optional surrounding whitespace, optional sign, then either a
 // decimal literal (digits with single underscores between digits, optional fraction and exponent) or
 // nan / inf / infinity in any case.  Returns false for anything Python would reject (hex, "nan(…)",
@@ -101,6 +176,7 @@ bool parse_py_float(const char* b, const char* e, double* out) {
   for (const char* q = p; q < e; ++q)
     if (*q != '_') dst[n++] = *q;
   dst[n] = 0;
+  if (fast_decimal(dst, dst + n, out)) return true;
   char* end = nullptr;
   *out = strtod(dst, &end);  // correctly rounded; overflow -> ±inf, underflow -> 0/subnormal, as CPython
   return end == dst + n;

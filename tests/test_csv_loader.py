@@ -174,3 +174,37 @@ def test_integration_md_csv_stub_runs(tmp_path, monkeypatch):
     assert ids == rids and t.dtype == torch.float16 and np.array_equal(t.numpy(), rx)
     with pytest.raises(FileNotFoundError):
         ns["load_data"](str(tmp_path / "nope.csv"), 8, [128])
+
+
+def _near_midpoint_strings(n=6000, seed=11):
+    """Decimal strings of 15-19 significant digits at and around the midpoints between adjacent
+    float32 values and between adjacent doubles: the inputs where a wrong str -> double rounding would
+    change the float32 that numpy produces (the double is cast to float32 afterwards)."""
+    from decimal import Decimal, getcontext
+    getcontext().prec = 80
+    rng = np.random.default_rng(seed)
+    f = (rng.standard_normal(n) * 10.0 ** rng.integers(-9, 9, n)).astype(np.float32)
+    out = []
+    for i, a in enumerate(f[: n // 2]):
+        b = np.nextafter(a, np.float32(np.inf))
+        mid = (Decimal(float(a)) + Decimal(float(b))) / 2
+        for digits in (15, 17, 19):
+            out.append(format(mid, f".{digits - 1}e"))
+        half_ulp = Decimal(float(np.spacing(float(mid)))) / 2
+        for k in (-1, 1):
+            out.append(format(mid + k * half_ulp, ".18e"))
+    for a in f[n // 2:]:
+        d = float(a) * (1 + 1e-9)
+        e = np.nextafter(d, np.inf)
+        mid = (Decimal(d) + Decimal(e)) / 2
+        out += [format(mid, ".18e"), format(mid, ".16e"), repr(d), f"{d:.9g}", f"{d:.12f}"]
+    return out
+
+
+def test_float_fast_path_matches_numpy(tmp_path):
+    vals = _near_midpoint_strings()
+    p = tmp_path / "m.csv"
+    p.write_text("".join(f"r{i},{v}\n" for i, v in enumerate(vals)))
+    ids, x = check(p, 1)
+    assert len(ids) == len(vals)
+    check(p, 1, (1280,))
