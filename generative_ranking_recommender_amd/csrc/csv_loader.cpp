@@ -43,8 +43,9 @@ struct Part {
 inline bool is_eol(char c) { return c == '\n' || c == '\r'; }
 inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\f' || c == '\v'; }
 
-// Correctly rounded decimal -> double for the common case, without strtod: s..e is a validated literal
-// (sign, digits, '.', exponent; no underscores).  With at most 19 significant digits the literal is
+// Correctly rounded decimal -> double for the common case, without strtod: s..e is a trimmed literal
+// [sign] digits [. digits] [(e|E) [sign] digits] with at least one mantissa digit (anything else, '_'
+// included, returns false and is left to the validating slow path).  With at most 19 significant digits the literal is
 // w 10^q exactly (w < 2^64).  |q| <= 22 and w <= 2^53: one IEEE operation on exact operands (Clinger).
 // |q| <= 27: x87 extended arithmetic (10^27 = 5^27 2^27 is exact in a 64-bit significand) gives w 10^q
 // within one unit of the 64-bit significand; rounding that to double is correct unless its 11 extra
@@ -56,7 +57,9 @@ bool fast_decimal(const char* s, const char* e, double* out) {
   if (s < e && (*s == '-' || *s == '+')) neg = *s++ == '-';
   uint64_t w = 0;
   int nd = 0, q = 0;
+  bool md = false;  // a mantissa digit seen
   for (; s < e && *s >= '0' && *s <= '9'; ++s) {
+    md = true;
     if (nd || *s != '0') {
       if (nd == 19) return false;
       w = w * 10 + (uint64_t)(*s - '0');
@@ -65,6 +68,7 @@ bool fast_decimal(const char* s, const char* e, double* out) {
   }
   if (s < e && *s == '.') {
     for (++s; s < e && *s >= '0' && *s <= '9'; ++s) {
+      md = true;
       if (nd || *s != '0') {
         if (nd == 19) return false;
         w = w * 10 + (uint64_t)(*s - '0');
@@ -73,10 +77,12 @@ bool fast_decimal(const char* s, const char* e, double* out) {
       --q;
     }
   }
+  if (!md) return false;
   if (s < e && (*s == 'e' || *s == 'E')) {
     ++s;
     bool eneg = false;
     if (s < e && (*s == '-' || *s == '+')) eneg = *s++ == '-';
+    if (s == e) return false;
     int x = 0;
     for (; s < e && *s >= '0' && *s <= '9'; ++s) {
       if (x > 10000) return false;
@@ -139,6 +145,7 @@ bool parse_py_float(const char* b, const char* e, double* out) {
       if ((p[i] | 0x20) != w[i]) return false;
     return true;
   };
+  if (((*p >= '0' && *p <= '9') || *p == '.') && fast_decimal(b, e, out)) return true;  // no copy
   if (ieq("nan")) { *out = neg ? -NAN : NAN; return true; }
   if (ieq("inf") || ieq("infinity")) { *out = neg ? -INFINITY : INFINITY; return true; }
   // decimal literal: [digits][.digits][(e|E)[sign]digits], at least one mantissa digit,
@@ -176,7 +183,7 @@ bool parse_py_float(const char* b, const char* e, double* out) {
   for (const char* q = p; q < e; ++q)
     if (*q != '_') dst[n++] = *q;
   dst[n] = 0;
-  if (fast_decimal(dst, dst + n, out)) return true;
+  if (fast_decimal(dst, dst + n, out)) return true;  // literals with '_'
   char* end = nullptr;
   *out = strtod(dst, &end);  // correctly rounded; overflow -> ±inf, underflow -> 0/subnormal, as CPython
   return end == dst + n;

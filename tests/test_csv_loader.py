@@ -208,3 +208,13 @@ def test_float_fast_path_matches_numpy(tmp_path):
     ids, x = check(p, 1)
     assert len(ids) == len(vals)
     check(p, 1, (1280,))
+
+
+def test_random_grammar_matches_python(tmp_path):
+    """Random short tokens over the literal alphabet: accepted / rejected and valued as numpy does."""
+    rng = np.random.default_rng(5)
+    alpha = list("0123456789") * 3 + list(".eE+-_ ")
+    toks = ["".join(rng.choice(alpha, rng.integers(1, 9))) for _ in range(4000)]
+    p = tmp_path / "g.csv"
+    p.write_text("".join(f"t{i},{t}\n" for i, t in enumerate(toks)))
+    check(p, 1)
