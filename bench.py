@@ -52,8 +52,11 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--codebooks", choices=("fitted", "sampled"), default=os.environ.get("BENCH_CODEBOOKS", "fitted"),
                     help="fitted: short K-Means fits on a sample (trained-model geometry); sampled: residual rows")
-    ap.add_argument("--traffic-json", default=str(REPO / "profiles" / "r1_traffic.json"),
-                    help="PMC HBM bytes per launch of this build (tools/pmc_traffic.sh); missing file -> traffic null")
+    ap.add_argument("--traffic-json", default=str(REPO / "bench_data" / "traffic.json"),
+                    help="PMC HBM bytes per launch of this build (tools/pmc_traffic.sh; shipped to the GPU box, "
+                         "unlike profiles/); missing file -> traffic null")
+    ap.add_argument("--parity-rows", type=int, default=2048,
+                    help="rows of the timed output checked against the exact CPU oracle after the run (0 = skip)")
     return ap.parse_args()
 
 
@@ -177,6 +180,18 @@ def cpu_baseline(cb, rows):
                       f"{dt:.2f} s"}
 
 
+def check_sample(x, out, cb, rows):
+    """The timed run's last output on an evenly spaced row sample vs the exact oracle (the checker only,
+    after the timed region): the IDs must be identical."""
+    from oracle import rq_oracle as O
+    idx = torch.linspace(0, x.shape[0] - 1, rows, device=x.device).long()
+    xs = x[idx].cpu().numpy()
+    got = out[idx].cpu().numpy()
+    ref = O.encode(xs, [cb["c0"], cb["c1"], cb["c2"]], NEED, cb["match"], residual_from_weighted=True, exact=True)
+    bad = int((got != ref).any(1).sum())
+    return {"rows_checked": rows, "mismatches": bad, "against": "oracle/rq_oracle.py encode(exact=True), evenly spaced rows"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -262,7 +277,17 @@ def main():
     dom = max((k for k in kern if k.startswith("assign")), key=lambda k: kern[k]["ms"])
     dk = kern[dom]
     traffic = level_traffic(args.traffic_json, int(dom[-1])) if os.environ.get("RQSID_SCREEN_VARIANT", "0") == "0" else None
-    roof = {"kernel": dom + " (rqsid_assign: fp16 MFMA screen kernel + exact re-score kernel)", "bound": "hbm",
+    # Which roof applies: the level's algorithmic intensity (2 K_eff D flop per 2052 B: 64-128 flop/B) puts
+    # its fp16 MFMA time at <= 6 % of its HBM time at the two peaks, so HBM is the roof; the PMC traffic
+    # (when present) says whether the kernel moves more than its algorithmic bytes.
+    keff = NEED[int(dom[-1])]
+    t_hbm = n * bytes_row / (HBM_PEAK_GBS * 1e9)
+    t_mfma = n * 2 * keff * D / (BF16_PEAK_TFLOPS * 1e12)
+    roof = {"kernel": dom + " (rqsid_assign: fp16 MFMA screen kernel + exact re-score kernel)",
+            "bound": "hbm" if t_hbm >= t_mfma else "mfma",
+            "bound_basis": f"algorithmic: {t_hbm * 1e3:.2f} ms of HBM at peak vs {t_mfma * 1e3:.3f} ms of fp16 MFMA at "
+                           f"peak per launch" + (f"; PMC traffic = {traffic / (n * bytes_row):.3f} x the algorithmic bytes"
+                                                 if traffic else "; no PMC traffic for this build"),
             "achieved": dk["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dk["hbm_frac"],
             "traffic": traffic, "traffic_unit": "bytes per launch",
             "traffic_source": (os.path.relpath(args.traffic_json, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
@@ -294,6 +319,8 @@ def main():
         "roofline": roof,
         "kernels": kern,
     }
+    if args.parity_rows > 0:
+        line["parity"] = check_sample(x, out, cb, args.parity_rows)
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
         line["cpu_baseline"] = cpu_baseline(cb, args.cpu_sample)
     if rank == 0:

@@ -16,7 +16,7 @@ PKG = Path(__file__).resolve().parent
 REPO = PKG.parent
 LIB_PATH = PKG / "librqsid.so"
 SRCS = [PKG / "csrc" / "rqsid.hip", PKG / "csrc" / "assign.hip", PKG / "csrc" / "assign_stream.hip",
-        PKG / "csrc" / "auction.hip"]
+        PKG / "csrc" / "assign_resident.hip", PKG / "csrc" / "auction.hip"]
 DEPS = SRCS + [PKG / "csrc" / "internal.h", PKG / "csrc" / "assign_common.h"]
 HEADER = REPO / "include" / "rqsid.h"
 # host-only I/O library (CSV reader): plain g++, no GPU code
@@ -80,10 +80,20 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = LIB_PATH.with_suffix(".so.tmp")
-    cmd = [hipcc, *HIPCC_FLAGS, "-o", str(tmp), *map(str, SRCS)]
+    objdir = PKG / "build"
+    objdir.mkdir(exist_ok=True)
+    compile_flags = [f for f in HIPCC_FLAGS if f != "-shared"]
+    objs = [objdir / (src.stem + ".o") for src in SRCS]
+    cmds = [[hipcc, *compile_flags, "-c", "-o", str(o), str(src)] for src, o in zip(SRCS, objs)]
     if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+        for c in cmds:
+            print(" ".join(c))
+    # one hipcc per translation unit, in parallel (the kernels are template-heavy: minutes serially)
+    procs = [subprocess.Popen(c) for c in cmds]
+    bad = [c for c, pr in zip(cmds, procs) if pr.wait() != 0]
+    if bad:
+        raise subprocess.CalledProcessError(1, bad[0])
+    subprocess.run([hipcc, *HIPCC_FLAGS, "-o", str(tmp), *map(str, objs)], check=True)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
 

@@ -900,9 +900,11 @@ int screen_variant() {  // read per call: tests switch it within one process
   return e ? atoi(e) : 0;
 }
 
-bool g_attr_done = false;
+bool g_attr_done[kMaxDevices] = {};
 int ensure_attrs() {
-  if (g_attr_done) return RQSID_OK;
+  const int dev = current_device();
+  if (dev < 0) return fail(RQSID_E_LAUNCH, "assign: hipGetDevice failed");
+  if (g_attr_done[dev]) return RQSID_OK;
   bool ok = true;
   set_attrs<4, 2, false, true>(&ok);
   set_attrs<8, 2, false, true>(&ok);
@@ -911,7 +913,7 @@ int ensure_attrs() {
   set_attrs<8, 2, false, false>(&ok);
   set_attrs<4, 2, true, false>(&ok);
   if (!ok) return fail(RQSID_E_LAUNCH, "assign: cannot raise the dynamic LDS limit");
-  g_attr_done = true;
+  g_attr_done[dev] = true;
   return RQSID_OK;
 }
 
@@ -958,10 +960,11 @@ int rqsid_prepare_centers(const float* centers, int64_t k, int32_t dim, uint16_t
 int32_t rqsid_assign_tile_rows(void) { return kTileRows; }
 
 // workspace: [0,256) counters and store sinks | WorkItem[n_rows] | tile->segment map i32[n_rows]
-// (tiles <= rows) | compact row list i32[n_rows]
+// (tiles <= rows) | compact row list i32[n_rows] (resident screen: 32-row tile offsets per segment) |
+// resident screen tile descriptors int4[n_rows]
 int64_t rqsid_assign_workspace_bytes(int64_t n_rows) {
   const int64_t n = n_rows > 0 ? n_rows : 0;
-  return 256 + n * (int64_t)sizeof(WorkItem) + 2 * ((n * 4 + 255) / 256 * 256);
+  return 256 + n * (int64_t)sizeof(WorkItem) + 2 * ((n * 4 + 255) / 256 * 256) + resident_desc_bytes(n);
 }
 
 int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row_index, int32_t n_segments,
@@ -1044,10 +1047,28 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   // Variant 1 forces the per-tile kernel, variant 5 the stream forms (RQSID_STREAM_SHAPE).
   const int variant = screen_variant();
   const int shape = variant == 5 ? 0 : (variant == 0 && nt == 8 && !t3 ? 88 : -1);
-  const bool use_stream = stream_ok && shape >= 0;
-  if (use_stream) {
+  const bool use_stream = stream_ok && shape >= 0 && variant != 6;
+  // the centre-resident screen (assign_resident.hip): variant 6 forces it wherever it applies (1-term,
+  // <= 256 candidates).  Not the default yet: measured L2 of the bench 8.0-9.1 ms against the ping-pong
+  // form's 7.6 ms ('Centre-resident screen')
+  const bool res_ok = resident_supported(dim, cand_count_max, t3, res_levels) && (int64_t)n_segments + 1 <= n_rows &&
+                      (res_levels != 1 || !norm || den_out);
+  const bool use_res = res_ok && variant == 6;
+  if (use_res) {
+    int4* desc = reinterpret_cast<int4*>(work_idx + (n_rows * 4 + 255) / 256 * 64);
+    // tile_seg's slot holds the segment of each ambiguous row
+    if ((rc = launch_resident_screen(p, t3, res_levels, norm, desc, work_idx, tile_seg, n_rows, st))) return rc;
+    // re-score rows carry the sentinel -2 and their pass masks at work[row] (the 32-row tile offsets in
+    // the compact-list area are dead by now); the expand pass makes them work items
+    hipLaunchKernelGGL(sentinel_compact_kernel, dim3((unsigned)cdiv(n_rows, kCompactRows)), dim3(256), 0, st, out_global,
+                       n_rows, p.work_count, work_idx);
+    p.work_idx = work_idx;
+    launch_resident_expand(p, tile_seg, t3, n_rows, st);
+  } else if (use_stream) {
     // the 256-row tile offsets live in the compact-list area until the compaction pass
-    launch_stream_screen(p, nt, t3, res_levels, norm, tile_seg, work_idx, n_rows, shape, st);
+    // a failed stream launch returns its status here: the compaction and re-score below must never run
+    // over an out_global the screen did not write
+    if ((rc = launch_stream_screen(p, nt, t3, res_levels, norm, tile_seg, work_idx, n_rows, shape, st))) return rc;
     if ((rc = check_launch("assign_stream"))) return rc;
     hipLaunchKernelGGL(sentinel_compact_kernel, dim3((unsigned)cdiv(n_rows, kCompactRows)), dim3(256), 0, st, out_global,
                        n_rows, p.work_count, work_idx);
@@ -1059,7 +1080,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
       p.tile_seg = tile_seg;
     }
   }
-  if (use_stream) {
+  if (use_stream || use_res) {
   } else if (t3) launch_screen2<4, 2, true>(p, res_levels, norm, grid, !legacy, st);
   else if (cand_count_max <= 128) launch_screen2<4, 2, false>(p, res_levels, norm, grid, !legacy, st);
   else if (cand_count_max <= 256) launch_screen2<8, 2, false>(p, res_levels, norm, grid, !legacy, st);

@@ -458,8 +458,17 @@ __device__ __forceinline__ void row_frag(const float4 xa, const float4 xc, const
 // table-wide epilogue constants written by rqsid_prepare_centers into meta row k:
 // {2^-s, max |ec2|/|c|, max |ec1|/|c|, max |c|} (rounded up)
 // shape: 88 ping-pong 8-wave form, 83 / 42 streamed 8x3 / 4x2 forms, 0 = RQSID_STREAM_SHAPE (default 83)
-void launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
-                          int32_t* seg_tile256, int64_t cap, int shape, hipStream_t st);
+int launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
+                         int32_t* seg_tile256, int64_t cap, int shape, hipStream_t st);
 bool stream_supported(int nt, bool t3, int rl, bool norm);
+
+// centre-resident screen (assign_resident.hip): 512-d rows, <= 256 candidates per segment (1 term) or
+// <= 128 (3 terms).  desc: resident_desc_bytes(n_rows) of workspace; seg_tile32: n_segments + 1 ints.
+bool resident_supported(int dim, int cand_count_max, bool t3, int rl);
+int64_t resident_desc_bytes(int64_t n_rows);
+int launch_resident_screen(const AssignParams& p, bool t3, int rl, bool norm, int4* desc, int32_t* seg_tile32,
+                           int32_t* seg_of_row, int64_t cap, hipStream_t st);
+// after the sentinel compaction: pass masks of the listed rows -> work items (p.work_idx set)
+void launch_resident_expand(const AssignParams& p, const int32_t* seg_of_row, bool t3, int64_t n_rows, hipStream_t st);
 
 }  // namespace rqsid

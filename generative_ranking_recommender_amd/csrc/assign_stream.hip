@@ -1131,19 +1131,14 @@ template <int NT, int RL, bool NORM, bool T3, int W, int S>
 bool launch_one(const AssignParams& p, const int32_t* tile_seg, const int32_t* seg_tiles, int64_t max_tiles,
                 hipStream_t st) {
   using L = StreamLayout<NT, RL, NORM, T3, W, S>;
-  static int ncu = 0;
-  static bool attr = false;
-  if (!ncu) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
-    ncu = prop.multiProcessorCount;
-  }
-  if (!attr) {
+  static bool attr[kMaxDevices] = {};
+  const int dev = current_device(), ncu = device_cu_count();
+  if (dev < 0 || !ncu) return false;
+  if (!attr[dev]) {
     if (hipFuncSetAttribute((const void*)assign_stream_kernel<NT, RL, NORM, T3, W, S>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, L::kBytes) != hipSuccess)
       return false;
-    attr = true;
+    attr[dev] = true;
   }
   int64_t g = (int64_t)ncu * L::kBlocks;  // persistent: every block resident at once
   if (g > max_tiles) g = max_tiles;
@@ -1166,19 +1161,14 @@ template <int NT, int RL, bool NORM, bool T3>
 bool launch_pp(const AssignParams& p, const int32_t* tile_seg, const int32_t* seg_tiles, int64_t max_tiles,
                hipStream_t st) {
   using L = PPLayout<NT, RL, NORM, T3>;
-  static int ncu = 0;
-  static bool attr = false;
-  if (!ncu) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
-    ncu = prop.multiProcessorCount;
-  }
-  if (!attr) {
+  static bool attr[kMaxDevices] = {};
+  const int dev = current_device(), ncu = device_cu_count();
+  if (dev < 0 || !ncu) return false;
+  if (!attr[dev]) {
     if (hipFuncSetAttribute((const void*)assign_pp_kernel<NT, RL, NORM, T3>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             L::kBytes) != hipSuccess)
       return false;
-    attr = true;
+    attr[dev] = true;
   }
   int64_t g = ncu;  // one persistent 8-wave block per CU
   if (g > max_tiles) g = max_tiles;
@@ -1189,14 +1179,14 @@ bool launch_pp(const AssignParams& p, const int32_t* tile_seg, const int32_t* se
   return true;
 }
 
-void launch_pp_shape(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles,
+bool launch_pp_shape(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles,
                      int64_t cap, hipStream_t st) {
   constexpr int R = 256;
   hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, R, seg_tiles);
   const int64_t max_tiles = cap / R + p.n_segments;
   const unsigned tg = (unsigned)(max_tiles / 256 + 1 < 4096 ? max_tiles / 256 + 1 : 4096);
   hipLaunchKernelGGL(tile_seg_kernel, dim3(tg), dim3(256), 0, st, seg_tiles, p.n_segments, cap, tile_seg);
-#define RQ_L(NT, RL, NORM, T3) launch_pp<NT, RL, NORM, T3>(p, tile_seg, seg_tiles, max_tiles, st)
+#define RQ_L(NT, RL, NORM, T3) return launch_pp<NT, RL, NORM, T3>(p, tile_seg, seg_tiles, max_tiles, st)
   if (nt == 8) {
     if (rl == 0) RQ_L(8, 0, false, false);
     else if (rl == 1) { if (norm) RQ_L(8, 1, true, false); else RQ_L(8, 1, false, false); }
@@ -1211,17 +1201,18 @@ void launch_pp_shape(const AssignParams& p, int nt, bool t3, int rl, bool norm, 
     else { if (norm) RQ_L(4, 2, true, false); else RQ_L(4, 2, false, false); }
   }
 #undef RQ_L
+  return false;
 }
 
 template <int W, int S>
-void launch_shape(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles,
+bool launch_shape(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles,
                   int64_t cap, hipStream_t st) {
   constexpr int R = W * 32;
   hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, R, seg_tiles);
   const int64_t max_tiles = cap / R + p.n_segments;  // bound on the R-row tiles
   const unsigned tg = (unsigned)(max_tiles / 256 + 1 < 4096 ? max_tiles / 256 + 1 : 4096);
   hipLaunchKernelGGL(tile_seg_kernel, dim3(tg), dim3(256), 0, st, seg_tiles, p.n_segments, cap, tile_seg);
-#define RQ_L(NT, RL, NORM, T3) launch_one<NT, RL, NORM, T3, W, S>(p, tile_seg, seg_tiles, max_tiles, st)
+#define RQ_L(NT, RL, NORM, T3) return launch_one<NT, RL, NORM, T3, W, S>(p, tile_seg, seg_tiles, max_tiles, st)
   if (nt == 8) {
     if (rl == 0) RQ_L(8, 0, false, false);
     else if (rl == 1) { if (norm) RQ_L(8, 1, true, false); else RQ_L(8, 1, false, false); }
@@ -1236,6 +1227,7 @@ void launch_shape(const AssignParams& p, int nt, bool t3, int rl, bool norm, int
     else { if (norm) RQ_L(4, 2, true, false); else RQ_L(4, 2, false, false); }
   }
 #undef RQ_L
+  return false;
 }
 
 }  // namespace
@@ -1247,12 +1239,14 @@ bool stream_supported(int nt, bool t3, int rl, bool norm) {
   return false;
 }
 
-void launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
-                          int32_t* seg_tiles, int64_t cap, int shape, hipStream_t st) {
+int launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
+                         int32_t* seg_tiles, int64_t cap, int shape, hipStream_t st) {
   if (shape == 0) shape = stream_shape();
-  if (shape == 88) launch_pp_shape(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
-  else if (shape == 42) launch_shape<4, 2>(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
-  else launch_shape<8, 3>(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
+  bool ok;
+  if (shape == 88) ok = launch_pp_shape(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
+  else if (shape == 42) ok = launch_shape<4, 2>(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
+  else ok = launch_shape<8, 3>(p, nt, t3, rl, norm, tile_seg, seg_tiles, cap, st);
+  return ok ? RQSID_OK : fail(RQSID_E_LAUNCH, "assign: stream screen launch failed (device query / LDS attribute)");
 }
 
 }  // namespace rqsid

@@ -13,6 +13,13 @@ int fail(int code, const char* fmt, ...);
 int check_launch(const char* what);
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Per-device one-time state (dynamic-LDS attributes, CU counts) is kept per HIP device: a kernel
+// attribute set on one device says nothing about another.  current_device() is -1 on error or
+// beyond kMaxDevices; device_cu_count() is cached per device (0 on error).
+constexpr int kMaxDevices = 64;
+int current_device();
+int device_cu_count();
 inline unsigned grid_cap(int64_t want, int64_t cap) {
   return (unsigned)(want < 1 ? 1 : (want > cap ? cap : want));
 }

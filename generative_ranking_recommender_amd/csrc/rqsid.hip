@@ -452,17 +452,37 @@ __global__ __launch_bounds__(256) void greedy_match_kernel(const float* __restri
   if (threadIdx.x == 0) n_sel[g] = tot[0] + tot[1] + tot[2] + tot[3];
 }
 
+int current_device() {
+  int d = -1;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDevices) return -1;
+  return d;
+}
+
+int device_cu_count() {
+  static int ncu[kMaxDevices] = {};
+  const int d = current_device();
+  if (d < 0) return 0;
+  if (!ncu[d]) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d) != hipSuccess) return 0;
+    ncu[d] = prop.multiProcessorCount;
+  }
+  return ncu[d];
+}
+
 namespace {
-bool g_attr_done = false;
+bool g_attr_done[kMaxDevices] = {};
 int ensure_attrs() {
-  if (g_attr_done) return RQSID_OK;
+  const int dev = current_device();
+  if (dev < 0) return fail(RQSID_E_LAUNCH, "hipGetDevice failed");
+  if (g_attr_done[dev]) return RQSID_OK;
   hipError_t e = hipFuncSetAttribute((const void*)bucket_hist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      kBucketLdsBins * 4);
   if (e != hipSuccess) return fail(RQSID_E_LAUNCH, "set smem attr (hist): %s", hipGetErrorString(e));
   e = hipFuncSetAttribute((const void*)bucket_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                           kBucketLdsBins * 4);
   if (e != hipSuccess) return fail(RQSID_E_LAUNCH, "set smem attr (scatter): %s", hipGetErrorString(e));
-  g_attr_done = true;
+  g_attr_done[dev] = true;
   return RQSID_OK;
 }
 }  // namespace
@@ -612,6 +632,19 @@ int rqsid_greedy_match(const float* dist, const int32_t* sub_off, int32_t groups
   if (!dist || !sub_off || !match || !n_selected || groups < 0 || n_cand <= 0 || n_cand > 65536 || max_take < 0)
     return fail(RQSID_E_ARG, "greedy_match: bad arguments (groups=%d C=%d)", groups, n_cand);
   if (groups == 0) return RQSID_OK;
+  // one byte of dynamic LDS per candidate column beside the kernel's static LDS: beyond the default
+  // 64 KiB the limit is raised (per device) up to the CU's 160 KiB
+  if (n_cand > 32768) {
+    static bool raised[kMaxDevices] = {};
+    const int dev = current_device();
+    if (dev < 0) return fail(RQSID_E_LAUNCH, "greedy_match: hipGetDevice failed");
+    if (!raised[dev]) {
+      if (hipFuncSetAttribute((const void*)greedy_match_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 65536) !=
+          hipSuccess)
+        return fail(RQSID_E_LAUNCH, "greedy_match: cannot raise the dynamic LDS limit");
+      raised[dev] = true;
+    }
+  }
   hipLaunchKernelGGL(greedy_match_kernel, dim3((unsigned)groups), dim3(256), (size_t)n_cand, (hipStream_t)stream, dist,
                      sub_off, n_cand, max_take, match, n_selected);
   return check_launch("greedy_match");

@@ -138,9 +138,14 @@ class RQEncoder:
         if self.sem.match_lookup:
             mult = self.need[l - 2] if self.sem.last_group_mult == "need_l_minus_2" else self.need[-2]
             grp = out[l - 2] * mult + out[l - 1]
-            if mult < self.need[l - 1] and int(grp.max().item()) >= self.n_groups:
-                raise IndexError(f"index {int(grp.max().item())} is out of bounds for axis 0 with size "
-                                 f"{self.n_groups}")
+            # the reference indexes match_matrix_np[before] (hierarchical_rq_kmeans.py:1279-1281) and raises
+            # IndexError past the last group; bucketing would silently drop such rows.  Check on the device
+            # values only when the largest possible id can reach it (never for the shipped presets:
+            # need[l-2] == need[l-1]), so the common encode has no host sync here.
+            if (self.need[l - 2] - 1) * mult + self.need[l - 1] - 1 >= self.n_groups:
+                gmax = int(grp.max().item())
+                if gmax >= self.n_groups:
+                    raise IndexError(f"index {gmax} is out of bounds for axis 0 with size {self.n_groups}")
             return ops.bucket(grp, self.n_groups)
         return ops.single_segment(n, device)
 

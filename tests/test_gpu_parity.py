@@ -317,6 +317,25 @@ def test_fused_residuals_equal_materialized(sem_name):
     assert torch.equal(a, b)
 
 
+def test_last_level_group_out_of_range_raises():
+    """need[0] > need[1]: the hierarchical before-id l0*need[0] + l1 can pass the need[0]*need[1] match
+    rows; the reference raises IndexError at match_matrix_np[before] (hierarchical_rq_kmeans.py:1279-1281),
+    and so must both encode paths (bucketing would silently drop the rows)."""
+    need = (32, 16, 32)
+    cb = synth.encode_codebooks(seed=7, need=need, n_cand=320, pool_rows=8192)
+    x = gpu(synth.mixture_rows(0, 8000))
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], list(need),
+                    match=torch.from_numpy(cb["match"]), semantics=HIERARCHICAL_TRAIN, device=DEV)
+    ids0 = O.nearest(synth.mixture_rows(0, 8000), cb["c0"])
+    assert ids0.max() * need[0] + need[1] - 1 >= need[0] * need[1]  # the input does reach past the last group
+    assert enc.fused
+    with pytest.raises(IndexError):
+        enc.encode(x)
+    enc.force_materialized = True
+    with pytest.raises(IndexError):
+        enc.encode(x)
+
+
 def test_multigroup_weighted_encode_vs_oracle():
     """group_dims [128, 384] with the reference's default weights 1/len(groups) (:56-62): the
     materialised path (scale_groups + per-group normalised residuals) vs the oracle."""
@@ -353,7 +372,8 @@ PER_TILE = {"RQSID_SCREEN_VARIANT": 1}
 STREAMED = {"default": {"RQSID_SCREEN_VARIANT": 0},
             "s83": {"RQSID_SCREEN_VARIANT": 5, "RQSID_STREAM_SHAPE": 83},
             "s42": {"RQSID_SCREEN_VARIANT": 5, "RQSID_STREAM_SHAPE": 42},
-            "pp88": {"RQSID_SCREEN_VARIANT": 5, "RQSID_STREAM_SHAPE": 88}}
+            "pp88": {"RQSID_SCREEN_VARIANT": 5, "RQSID_STREAM_SHAPE": 88},
+            "res": {"RQSID_SCREEN_VARIANT": 6}}  # the centre-resident screen wherever it applies
 
 
 @pytest.mark.parametrize("form", list(STREAMED))
@@ -386,7 +406,7 @@ def test_stream_kernel_equals_tile_kernel(shape, sem_name, form):
     assert (a[sel] == ref).all()
 
 
-@pytest.mark.parametrize("form", ["default", "s83", "pp88"])
+@pytest.mark.parametrize("form", ["default", "s83", "pp88", "res"])
 @pytest.mark.parametrize("k", [100, 128, 200, 256])
 def test_stream_nearest_partial_tiles(k, form):
     """Single-segment nearest with k < NT*32 candidates (padding lanes masked) on the streamed path."""

@@ -194,3 +194,28 @@ def test_sharded_lloyd_on_gpu_world1(tmp_path):
         torch.testing.assert_close(sl.cluster_centers, km.cluster_centers, rtol=1e-6, atol=1e-6)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_cand", [300, 65536])
+def test_greedy_match_matches_numpy(n_cand):
+    """rqsid_greedy_match (the match-matrix builders' greedy unique-nearest step) against a numpy
+    restatement of _assign_last_match_matrix :1022-1038, up to the largest accepted column count
+    (65536 columns = 64 KiB of dynamic LDS per group)."""
+    rng = np.random.default_rng(n_cand)
+    sizes = [5, 0, 9, 3]
+    sub_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    dist = rng.random((int(sub_off[-1]), n_cand), dtype=np.float32)
+    dist[2, :] = dist[1, :]  # duplicate rows: the second takes the next-nearest free column
+    max_take = 4
+    got, nsel = ops.greedy_match(torch.from_numpy(dist).cuda(), torch.from_numpy(sub_off).cuda(), max_take)
+    got = got.cpu().numpy()
+    want = np.zeros((len(sizes), n_cand), dtype=np.uint8)
+    for g in range(len(sizes)):
+        used = np.zeros(n_cand, bool)
+        for r in range(sub_off[g], sub_off[g] + min(sizes[g], max_take)):
+            d = np.where(used, np.inf, dist[r])
+            c = int(np.argmin(d))
+            used[c] = True
+            want[g, c] = 1
+    assert (got == want).all()
+    assert (nsel.cpu().numpy() == want.sum(1)).all()
