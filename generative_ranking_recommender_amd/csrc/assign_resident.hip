@@ -44,6 +44,9 @@ namespace {
 #ifndef RQ_PF
 #define RQ_PF 2  // fragment prefetch distance (k-steps)
 #endif
+#ifndef RQ_ILV
+#define RQ_ILV 0  // A/B: VALU instructions pinned after each MFMA of the fused block (0: compiler's order)
+#endif
 constexpr int kRD = 512;                 // row width of this kernel
 constexpr int kRT = 32;                  // rows per tile (the MFMA's N)
 constexpr int kKS = kRD / 16;            // k-steps of v_mfma_f32_32x32x16_f16
@@ -393,6 +396,16 @@ __global__ __launch_bounds__(512, 1) void assign_resident_kernel(AssignParams p,
           issue_row(rid2, ks / (kKS / 4));
         }
       }
+#if RQ_ILV > 0
+      // interleave: every MFMA followed by RQ_ILV VALU instructions of the producer (and one fragment
+      // read), so the matrix pipe runs under the producer within the wave
+#pragma unroll
+      for (int i = 0; i < kKS * (TWO ? 2 : 1); ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, RQ_ILV, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+#endif
     };
 #ifdef RQSID_STAMPS
     asm volatile("" ::"v"(R[0][0]), "v"(R[0][1]), "v"(R[1][0]), "v"(R[1][1]), "v"(R[2][0]), "v"(R[2][1]), "v"(R[3][0]), "v"(R[3][1]));

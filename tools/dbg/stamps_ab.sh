@@ -5,6 +5,6 @@ timeout -k 10 300 python tools/screen_sweep.py > $O/sweep.log 2>&1 || { tail $O/
 tail -1 $O/sweep.log
 for lib in ${LIBS}; do
   echo "== $lib"
-  RQSID_LIB=$lib timeout -k 10 300 python tools/res_stamps.py > $O/$(basename $lib).log 2>&1 || { tail $O/$(basename $lib).log; exit 1; }
+  RQSID_SCREEN_VARIANT=6 RQSID_LIB=$lib timeout -k 10 300 python tools/res_stamps.py > $O/$(basename $lib).log 2>&1 || { tail $O/$(basename $lib).log; exit 1; }
   grep L2 $O/$(basename $lib).log
 done
