@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--traffic-json", default=str(REPO / "bench_data" / "traffic.json"),
                     help="PMC HBM bytes per launch of this build (tools/pmc_traffic.sh; shipped to the GPU box, "
                          "unlike profiles/); missing file -> traffic null")
+    ap.add_argument("--train-iters", type=int, default=3,
+                    help="Lloyd iterations timed for the 'train' field (0 = skip)")
     ap.add_argument("--parity-rows", type=int, default=2048,
                     help="rows of the timed output checked against the exact CPU oracle after the run (0 = skip)")
     return ap.parse_args()
@@ -178,6 +180,42 @@ def cpu_baseline(cb, rows):
     return {"value": rows / dt, "unit": "vectors/s", "cores": int(threads), "kind": "port",
             "sample": f"{rows} rows x 3 levels, oracle/rq_oracle.py encode (numpy fp32 BLAS, {threads} threads), "
                       f"{dt:.2f} s"}
+
+
+def train_iterations(x, c0, iters, world, n_global):
+    """§8(d)'s training unit: rows x Lloyd iterations at level 0 (K = 128, unbalanced KMeans.fit step,
+    balancekmeans/__init__.py:368-465): exact assign (rqsid_assign) + fp64 per-cluster sums and counts
+    (rqsid_centroid_accumulate) + the mean update; with N > 1 the sums go through one RCCL all_reduce of
+    the fused [K*D + K] fp64 buffer (distributed.ShardedLloyd).  Timed after the encode, outside its
+    timed region; returns (ms per iteration (max over ranks), rows per second over all ranks)."""
+    from generative_ranking_recommender_amd.distributed import ShardedLloyd
+    k = c0.shape[0]
+    if world > 1:
+        import torch.distributed as tdist
+        lloyd = ShardedLloyd(k, x, n_global)
+
+        def step(c):
+            return lloyd.step(c)[0]
+    else:
+        def step(c):
+            a = ops.nearest(x, ops.prepare_centers(c))
+            return ops.centroid_update(x, a, k, c.clone())[0]
+    c = c0.clone()
+    c = step(c)  # warm-up (workspaces, LDS attributes)
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+    t = time.perf_counter()
+    for _ in range(iters):
+        c = step(c)
+    torch.cuda.synchronize()
+    if world > 1:
+        tdist.barrier()
+    el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=x.device)
+    if world > 1:
+        tdist.all_reduce(el, op=tdist.ReduceOp.MAX)
+    dt = float(el.item())
+    return dt / iters * 1e3, n_global * iters / dt
 
 
 def check_sample(x, out, cb, rows):
@@ -319,6 +357,12 @@ def main():
         "roofline": roof,
         "kernels": kern,
     }
+    if args.train_iters > 0:
+        t_ms, rps = train_iterations(x, torch.from_numpy(cb["c0"]).to(dev).float(), args.train_iters, world, n * world)
+        line["train"] = {"metric": "rows x Lloyd iterations/sec (level 0, K=128: assign + fp64 centroid update"
+                                   + (", RCCL all_reduce of the [K*D+K] sums" if world > 1 else "") + ")",
+                         "value": round(rps, 1), "unit": "rows/s", "ms_per_iteration": round(t_ms, 3),
+                         "iterations": args.train_iters, "rows": n * world}
     if args.parity_rows > 0:
         line["parity"] = check_sample(x, out, cb, args.parity_rows)
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostics (GPU, stamps build: EXTRA=-DRQSID_STAMPS MODES=0 tools/ab_build.sh): per encode level, the
-warp-specialised resident screen's cycles per tile for candidate wave 0 and producer wave 8, by phase."""
+centre-resident screen's cycles per tile for wave 0 (produces first) and wave 4 (multiplies first), by phase."""
 import ctypes
 import os
 import sys
@@ -15,9 +15,7 @@ from generative_ranking_recommender_amd import _lib, ops  # noqa: E402
 import generative_ranking_recommender_amd.encode as encmod  # noqa: E402
 from generative_ranking_recommender_amd.encode import HIERARCHICAL_TRAIN, RQEncoder  # noqa: E402
 
-PH = {0: {0: "loop", 1: "info", 2: "mfma", 3: "reload", 4: "epi1", 5: "barrier", 8: "e2_U", 9: "e2_pass",
-          10: "e2_store", 6: "e2_amb"},
-      1: {0: "loop", 1: "segprep", 2: "produce", 5: "barrier"}}
+PH = ["loop", "segchange", "fused", "reload", "barA", "barB", "decide", "tiles", "rowwait", "epi1", "epi2"]
 
 
 def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000))):
@@ -52,8 +50,9 @@ def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000))):
             tiles = max(w[7], 1)
             if w[0] == 0:
                 continue
-            parts = " ".join(f"{name}={w[k] / tiles:.0f}" for k, name in PH[role].items())
-            print(f"L{lvl} {'producer' if role else 'candidate'}: cycles/tile {parts}  (tiles {w[7]})", flush=True)
+            ks = [0, 1, 8, 2, 3, 9, 4, 10, 5, 6]
+            parts = " ".join(f"{PH[k]}={w[k] / tiles:.0f}" for k in ks)
+            print(f"L{lvl} wave{4 * role}: cycles/tile {parts}  (tiles {w[7]})", flush=True)
 
 
 if __name__ == "__main__":
