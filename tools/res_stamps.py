@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostics (GPU, stamps build: EXTRA=-DRQSID_STAMPS MODES=0 tools/ab_build.sh): per encode level, the
-centre-resident screen's cycles per tile for wave 0 (produces first) and wave 4 (multiplies first), by phase."""
+warp-specialised resident screen's cycles per tile for candidate wave 0 and producer wave 8, by phase."""
 import ctypes
 import os
 import sys
@@ -15,7 +15,8 @@ from generative_ranking_recommender_amd import _lib, ops  # noqa: E402
 import generative_ranking_recommender_amd.encode as encmod  # noqa: E402
 from generative_ranking_recommender_amd.encode import HIERARCHICAL_TRAIN, RQEncoder  # noqa: E402
 
-PH = ["loop", "segchange", "fused", "reload", "barA", "barB", "decide", "tiles", "rowwait", "epi1", "epi2"]
+PH = {0: {0: "loop", 1: "wait_ready", 2: "mfma", 3: "reload", 4: "epi1", 5: "wait_posted", 6: "epi2"},
+      1: {0: "loop", 1: "wait_consumed", 2: "segprep", 3: "produce"}}
 
 
 def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000))):
@@ -50,9 +51,8 @@ def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000))):
             tiles = max(w[7], 1)
             if w[0] == 0:
                 continue
-            ks = [0, 1, 8, 2, 3, 9, 4, 10, 5, 6]
-            parts = " ".join(f"{PH[k]}={w[k] / tiles:.0f}" for k in ks)
-            print(f"L{lvl} wave{4 * role}: cycles/tile {parts}  (tiles {w[7]})", flush=True)
+            parts = " ".join(f"{name}={w[k] / tiles:.0f}" for k, name in PH[role].items())
+            print(f"L{lvl} {'producer' if role else 'candidate'}: cycles/tile {parts}  (tiles {w[7]})", flush=True)
 
 
 if __name__ == "__main__":
