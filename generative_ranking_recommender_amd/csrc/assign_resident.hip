@@ -55,8 +55,17 @@ constexpr int kPW = 4;                   // producer waves
 constexpr int kRPW = kRT / kPW;          // rows per producer wave per tile
 constexpr int kThreads = (kCW + kPW) * 64;
 constexpr int kNC = kCW * 32;            // candidate capacity
+#ifndef RQ_DEFER
+#define RQ_DEFER 1  // epilogue 2 of tile j-1 after tile j's MFMAs
+#endif
+#ifndef RQ_LBF16
+#define RQ_LBF16 1  // deferred lower bounds as bf16 pairs rounded down
+#endif
+#ifndef RQ_NT
+#define RQ_NT 1  // non-temporal row loads (read once)
+#endif
 #ifndef RQ_LA
-#define RQ_LA 4  // k-steps of the centres kept in LDS (wave-private) instead of registers
+#define RQ_LA 6  // k-steps of the centres kept in LDS (wave-private) instead of registers
 #endif
 constexpr int kLA = RQ_LA;
 constexpr int kKR = kKS - kLA;           // k-steps held in registers
@@ -73,7 +82,7 @@ template <int RL>
 struct ResLayout {
   static constexpr int kNS = 4;                          // statistics buffers (drift bound 3)
   static constexpr int kNM = 3;                          // segment-metadata slots (drift bound 3)
-  static constexpr int kNE = 4;                          // exchange buffers (drift bound 3)
+  static constexpr int kNE = 3;                          // exchange buffers (drift bound 3)
   static constexpr int kStat = 2 * kImg;                 // [kNS][32 rows] float4 {m2, A2, row id, -}
   static constexpr int kCsq = kStat + kNS * kRT * 16;    // [kNM][kNC] |c|^2 (inf: padding)
   static constexpr int kCy = kCsq + kNM * kNC * 4;       // [kNM][kNC] |c|
@@ -84,8 +93,8 @@ struct ResLayout {
   static constexpr int kIds = kExch + kNE * kRT * kEX * 16;  // [kNE][32 rows][kEX] int2 {global, local} id of each wave's best
   static constexpr int kMask = kIds + kNE * kRT * kEX * 8;   // [2][32 rows][kCW] u32 pass masks of ambiguous rows
   static constexpr int kInfo = kMask + 2 * kRT * kCW * 4;   // [4 tiles][8] int tile-info ring
-  static constexpr int kCtr = kInfo + 4 * 8 * 4;         // counters {ready, consumed, posted, -}
-  static constexpr int kAL = kCtr + 16;                  // [kCW waves][kLA k-steps][64 lanes] f16x8 centre fragments
+  static constexpr int kCtr = kInfo + 4 * 8 * 4;         // per-wave counters: ready [4], -, consumed [8], posted [8]
+  static constexpr int kAL = kCtr + 24 * 4 + 32;         // [kCW waves][kLA k-steps][64 lanes] f16x8 centre fragments
   static constexpr int kBytes = kAL + kCW * kLA * 64 * 16;
   static_assert(kBytes <= 160 * 1024, "LDS budget");
 };
@@ -110,15 +119,6 @@ __device__ __forceinline__ ResSeg res_seg(const AssignParams& p, int s) {
 // does not see them: the producers' rare segment preparation, written with these, leaves the loop
 // without conditional vector loads, whose path-insensitive counting would otherwise put a full drain
 // of the row stream in every iteration.  (The drain here happens on segment changes only.)
-__device__ __forceinline__ void ld4_sync(int (&v)[4], const int32_t* a0, const int32_t* a1, const int32_t* a2,
-                                         const int32_t* a3) {
-  asm volatile(
-      "global_load_dword %0, %4, off\n\tglobal_load_dword %1, %5, off\n\t"
-      "global_load_dword %2, %6, off\n\tglobal_load_dword %3, %7, off\n\ts_waitcnt vmcnt(0)"
-      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
-      : "v"(a0), "v"(a1), "v"(a2), "v"(a3)
-      : "memory");
-}
 __device__ __forceinline__ void ldf4x4_sync(float4 (&v)[4], const float4* a0, const float4* a1, const float4* a2,
                                             const float4* a3) {
   typedef __attribute__((ext_vector_type(4))) float f4;
@@ -134,52 +134,84 @@ __device__ __forceinline__ void ldf4x4_sync(float4 (&v)[4], const float4* a0, co
   v[2] = make_float4(t2.x, t2.y, t2.z, t2.w);
   v[3] = make_float4(t3.x, t3.y, t3.z, t3.w);
 }
-__device__ __forceinline__ float4 ldf4_sync(const float4* a) {
-  typedef __attribute__((ext_vector_type(4))) float f4;
-  f4 t;
-  asm volatile("global_load_dwordx4 %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(t) : "v"(a) : "memory");
-  return make_float4(t.x, t.y, t.z, t.w);
-}
 
 // res_seg through ld4_sync (the producers' loop)
 __device__ __forceinline__ ResSeg res_seg_sync(const AssignParams& p, int s) {
-  int v[4], f;
-  ld4_sync(v, p.cand_count + s, p.cand_base + s, p.seg_ca ? p.seg_ca + s : p.cand_count + s,
-           p.seg_cb ? p.seg_cb + s : p.cand_count + s);
-  const uint8_t* fb = p.seg_flags ? p.seg_flags + s : reinterpret_cast<const uint8_t*>(p.cand_count + s);
-  asm volatile("global_load_ubyte %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(f) : "v"(fb) : "memory");
+  const int32_t* a0 = p.cand_count + s;
+  const int32_t* a1 = p.cand_base + s;
+  const int32_t* a2 = p.seg_ca ? p.seg_ca + s : a0;
+  const int32_t* a3 = p.seg_cb ? p.seg_cb + s : a0;
+  const uint8_t* fb = p.seg_flags ? p.seg_flags + s : reinterpret_cast<const uint8_t*>(a0);
+  int v0, v1, v2, v3, f;
+  asm volatile(
+      "global_load_dword %0, %5, off\n\tglobal_load_dword %1, %6, off\n\tglobal_load_dword %2, %7, off\n\t"
+      "global_load_dword %3, %8, off\n\tglobal_load_ubyte %4, %9, off\n\ts_waitcnt vmcnt(0)"
+      : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(f)
+      : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(fb)
+      : "memory");
   ResSeg g;
   g.s = s;
-  g.cnt = runi(v[0]);
-  g.cbase = runi(v[1]);
+  g.cnt = runi(v0);
+  g.cbase = runi(v1);
   const bool flag = p.seg_flags && (runi(f) & RQSID_SEG_PENALTY);
   g.pen = flag ? 2 : (g.cnt <= 0 ? 3 : 0);
-  g.ca = p.seg_ca ? runi(v[2]) : s;
-  g.cb = p.seg_cb ? runi(v[3]) : s;
+  g.ca = p.seg_ca ? runi(v2) : s;
+  g.cb = p.seg_cb ? runi(v3) : s;
   return g;
+}
+
+// a segment's candidate list words (4 cand_idx + 4 cand_lid per lane) and residual centre rows (4
+// float4 per lane) in one round trip
+__device__ __forceinline__ void ld_seg_sync(int (&ci)[4], int (&cl)[4], float4 (&rr)[4], const int32_t* const (&ia)[4],
+                                            const int32_t* const (&la)[4], const float4* const (&ra)[4]) {
+  typedef __attribute__((ext_vector_type(4))) float f4;
+  f4 r0, r1, r2, r3;
+  asm volatile(
+      "global_load_dword %0, %12, off\n\tglobal_load_dword %1, %13, off\n\t"
+      "global_load_dword %2, %14, off\n\tglobal_load_dword %3, %15, off\n\t"
+      "global_load_dword %4, %16, off\n\tglobal_load_dword %5, %17, off\n\t"
+      "global_load_dword %6, %18, off\n\tglobal_load_dword %7, %19, off\n\t"
+      "global_load_dwordx4 %8, %20, off\n\tglobal_load_dwordx4 %9, %21, off\n\t"
+      "global_load_dwordx4 %10, %22, off\n\tglobal_load_dwordx4 %11, %23, off\n\ts_waitcnt vmcnt(0)"
+      : "=&v"(ci[0]), "=&v"(ci[1]), "=&v"(ci[2]), "=&v"(ci[3]), "=&v"(cl[0]), "=&v"(cl[1]), "=&v"(cl[2]), "=&v"(cl[3]),
+        "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
+      : "v"(ia[0]), "v"(ia[1]), "v"(ia[2]), "v"(ia[3]), "v"(la[0]), "v"(la[1]), "v"(la[2]), "v"(la[3]), "v"(ra[0]),
+        "v"(ra[1]), "v"(ra[2]), "v"(ra[3])
+      : "memory");
+  rr[0] = make_float4(r0.x, r0.y, r0.z, r0.w);
+  rr[1] = make_float4(r1.x, r1.y, r1.z, r1.w);
+  rr[2] = make_float4(r2.x, r2.y, r2.z, r2.w);
+  rr[3] = make_float4(r3.x, r3.y, r3.z, r3.w);
 }
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Role signalling through monotonic LDS counters.  Signal: this wave's LDS writes complete
-// (lgkmcnt(0); the LDS performs a wave's operations in order), then lane 0 adds 1.  Wait: spin on the
-// counter (s_sleep between reads) until it reaches the target; the asm memory clobbers keep the
-// compiler from moving LDS accesses across either.  Vector-memory counts are untouched (no fence):
-// the roles exchange LDS data only.
+// Role signalling through per-wave monotonic LDS counters: each wave publishes how many tiles it has
+// finished a phase for (ready: producers; consumed, posted: candidates) in its own word, and a waiter
+// takes the minimum over the waves it depends on.  (A sum over waves would be wrong: waves of a role
+// drift, so a fast wave's extra tile can complete a sum while a slow wave is still mid-tile.)
+// Publish: this wave's LDS writes complete (lgkmcnt(0); the LDS performs a wave's operations in order),
+// then the new count.  Wait: spin (s_sleep between reads) until every counter reaches the target; the
+// asm memory clobbers keep the compiler from moving LDS accesses across either.  Vector-memory counts
+// are untouched (no fence): the roles exchange LDS data only.
 constexpr int kSpinCap = 1 << 20;  // ~0.1 s: far beyond any legitimate wait
 // ``dead`` (wave-uniform): set by a wait that reached the cap; later waits of the wave return at once,
 // so even a broken protocol ends the kernel in about one capped wait per wave (with wrong results)
-__device__ __forceinline__ void lds_signal(uint32_t* ctr, int lane) {
+__device__ __forceinline__ void lds_publish(uint32_t* own, uint32_t count) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (lane == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  *reinterpret_cast<volatile uint32_t*>(own) = count;
   asm volatile("" ::: "memory");
 }
-__device__ __forceinline__ void lds_wait_ge(const uint32_t* ctr, uint32_t target, int& dead) {
+template <int N>  // N = 4 or 8 counters, 16-B aligned
+__device__ __forceinline__ void lds_wait_all(const uint32_t* ctr, uint32_t target, int& dead) {
   int spin = dead ? kSpinCap : 0;
   for (; spin < kSpinCap; ++spin) {
     asm volatile("" ::: "memory");
-    const uint32_t v = (uint32_t)runi((int)__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (v >= target) break;
+    const volatile uint32_t* c = ctr;
+    uint32_t m = c[0];
+#pragma unroll
+    for (int i = 1; i < N; ++i) m = min(m, (uint32_t)c[i]);
+    if ((uint32_t)runi((int)m) >= target) break;
     __builtin_amdgcn_s_sleep(1);
   }
   dead = spin >= kSpinCap ? 1 : dead;
@@ -231,10 +263,10 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
   int32_t* const clid_base = reinterpret_cast<int32_t*>(smem + L::kClid);
   float4* const exch = reinterpret_cast<float4*>(smem + L::kExch);
   int32_t* const info = reinterpret_cast<int32_t*>(smem + L::kInfo);
-  uint32_t* const ctr_ready = reinterpret_cast<uint32_t*>(smem + L::kCtr);
-  uint32_t* const ctr_consumed = ctr_ready + 1;
-  uint32_t* const ctr_posted = ctr_ready + 2;
-  if (tid < 4) ctr_ready[tid] = 0;
+  uint32_t* const ctr_ready = reinterpret_cast<uint32_t*>(smem + L::kCtr);  // [kPW]
+  uint32_t* const ctr_consumed = ctr_ready + 8;                              // [kCW]
+  uint32_t* const ctr_posted = ctr_ready + 16;                               // [kCW]
+  if (tid < 24) ctr_ready[tid] = 0;
   lds_barrier();  // the only barrier: counters zeroed
   int dead = 0;
 
@@ -279,8 +311,13 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
       rrow[r] = __builtin_amdgcn_readlane(rid, r);
       const f4v* xr = reinterpret_cast<const f4v*>(p.x + (int64_t)rrow[r] * kRD);
 #ifndef RQ_AB_NOLOAD
+#if RQ_NT
       R[r][0] = __builtin_nontemporal_load(xr + lane);
       R[r][1] = __builtin_nontemporal_load(xr + 64 + lane);
+#else
+      R[r][0] = xr[lane];
+      R[r][1] = xr[64 + lane];
+#endif
 #else
       (void)xr;
       R[r][0] += 1.0f;
@@ -292,35 +329,36 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
       return (RL >= 2 && NORM) ? p.den_in[rid] : 1.0f;
     };
     // the segment's residual centre rows in registers (lane: dims 4l..4l+3 and 256+4l..): ca, cb
-    float4 cres[2][2];
-    auto load_res_rows = [&](const ResSeg& g) __attribute__((always_inline)) {
-      if (RL == 0) return;
-      const float4* ca = reinterpret_cast<const float4*>(p.ca + (int64_t)g.ca * kRD);
-      const float4* cb = RL >= 2 ? reinterpret_cast<const float4*>(p.cb + (int64_t)g.cb * kRD) : ca;
-      float4 v[4];
-      ldf4x4_sync(v, ca + lane, ca + 64 + lane, cb + lane, cb + 64 + lane);
-      cres[0][0] = v[0];
-      cres[0][1] = v[1];
-      cres[1][0] = v[2];
-      cres[1][1] = v[3];
-    };
-    // candidate |c|^2, |c| and ids of segment g -> metadata slot sl (this wave: list positions 64 pw ..),
-    // the collapsed bound's segment maxima -> sgz, sgy (every producer wave: all positions)
+    float4 cres[2][2] = {};
+    // Segment preparation in two round trips: (1) the candidate list words and the residual centre
+    // rows, (2) the candidates' c_meta.  Then: |c|^2, |c| and ids -> metadata slot sl (this wave: list
+    // positions 64 pw ..), the collapsed bound's segment maxima -> sgz, sgy (every producer wave: all
+    // positions), the residual rows -> cres.
     float sgz = 0.f, sgy = 0.f;
-    auto write_cmeta = [&](const ResSeg& g, int sl) __attribute__((always_inline)) {
-      float gz = 0.f, gy = 0.f;
-      if (g.cnt > 0) {
-        int kl[kPW], cg[kPW], lid[kPW];
-        const int32_t* ia[kPW];
-        const int32_t* la[kPW];
+    auto prep_segment = [&](const ResSeg& g, int sl) __attribute__((always_inline)) {
+      const bool any = g.cnt > 0;
+      int kl[kPW], cg[kPW], lid[kPW];
+      const int32_t* ia[kPW];
+      const int32_t* la[kPW];
 #pragma unroll
-        for (int q = 0; q < kPW; ++q) {
-          kl[q] = min(64 * q + lane, g.cnt - 1);
-          ia[q] = p.cand_idx ? p.cand_idx + g.cbase + kl[q] : p.cand_count;  // (stand-in: any valid word)
-          la[q] = p.cand_lid ? p.cand_lid + g.cbase + kl[q] : p.cand_count;
-        }
-        ld4_sync(cg, ia[0], ia[1], ia[2], ia[3]);
-        ld4_sync(lid, la[0], la[1], la[2], la[3]);
+      for (int q = 0; q < kPW; ++q) {
+        kl[q] = any ? min(64 * q + lane, g.cnt - 1) : 0;
+        ia[q] = p.cand_idx && any ? p.cand_idx + g.cbase + kl[q] : p.cand_count;  // (stand-in: any valid word)
+        la[q] = p.cand_lid && any ? p.cand_lid + g.cbase + kl[q] : p.cand_count;
+      }
+      const float4* stand = reinterpret_cast<const float4*>(p.c_meta);
+      const float4* ca = RL >= 1 ? reinterpret_cast<const float4*>(p.ca + (int64_t)g.ca * kRD) : stand;
+      const float4* cb = RL >= 2 ? reinterpret_cast<const float4*>(p.cb + (int64_t)g.cb * kRD) : stand;
+      const float4* ra[4] = {RL >= 1 ? ca + lane : stand, RL >= 1 ? ca + 64 + lane : stand,
+                             RL >= 2 ? cb + lane : stand, RL >= 2 ? cb + 64 + lane : stand};
+      float4 rr[4];
+      ld_seg_sync(cg, lid, rr, ia, la, ra);
+      cres[0][0] = rr[0];
+      cres[0][1] = rr[1];
+      cres[1][0] = rr[2];
+      cres[1][1] = rr[3];
+      float gz = 0.f, gy = 0.f;
+      if (any) {
         const float4* ma[kPW];
 #pragma unroll
         for (int q = 0; q < kPW; ++q) {
@@ -446,8 +484,7 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
       g1 = res_seg_sync(p, d1.x);
       slot1 = 1;
     }
-    load_res_rows(g0);
-    write_cmeta(g0, slot0);
+    prep_segment(g0, slot0);
     write_info(tb, g0, slot0);
     write_info(tb + 1, g1, slot1);
     const int rid1 = load_rids(d1);
@@ -465,7 +502,7 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
     int4 d3raw = desc_of(min(tb + 3, te - 1));
 #pragma unroll
     for (int r = 0; r < kRPW; ++r) issue_row(rid1, r);
-    lds_signal(ctr_ready, lane);  // tile tb (and info tb, tb+1, the metadata of its segment)
+    lds_publish(ctr_ready + pw, 1);  // tile tb (and info tb, tb+1, the metadata of its segment)
     // ---- steady state: iteration j produces tile j+1.  Vector loads per iteration, always the same
     // and in this order (counted waits stay exact and never drain the row stream): the descriptor of
     // tile j+3 and the row ids of tile j+2... issued before the rows; segment preparation loads through
@@ -480,7 +517,7 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
       // every candidate wave is done with tile j-1's MFMAs (so with its image buffer, which tile j+1
       // reuses) and, before them, with tile j-2's epilogue: the metadata slot, statistics buffer and
       // info entry written below are free
-      lds_wait_ge(ctr_consumed, (uint32_t)(kCW * it), dead);
+      lds_wait_all<kCW>(ctr_consumed, (uint32_t)it, dead);
       RS_MARK(1);
       // segment of tile j+2 (tile info for the candidate waves); tile j+1's: metadata, maxima and
       // residual rows, first needed by its production below
@@ -491,10 +528,7 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
         slot2 = slot1 == L::kNM - 1 ? 0 : slot1 + 1;
       }
       write_info(j + 2, g2, slot2);
-      if (has1 && d1.x != d0.x) {
-        write_cmeta(g1, slot1);
-        load_res_rows(g1);
-      }
+      if (has1 && d1.x != d0.x) prep_segment(g1, slot1);
       RS_MARK(2);
       // tile j+1: produce from R, re-fill R with tile j+2
 #pragma unroll
@@ -503,7 +537,7 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
         issue_row(rid2, r);
       }
       finish_rows(d1, (it + 1) & (L::kNS - 1), has1);
-      lds_signal(ctr_ready, lane);
+      lds_publish(ctr_ready + pw, (uint32_t)(it + 2));  // tiles tb .. j+1
       RS_MARK(3);
       d0 = d1;
       d1 = d2;
@@ -554,10 +588,95 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
         dst[1] = src[1];
       }
     };
+    // Epilogue 2 of tile j-1 runs after tile j's MFMAs (its inputs: the exchange of tile j-1, the row
+    // ids and lower bounds below, the tile's segment): the eight waves then meet only loosely (every
+    // wave has long posted j-1 when any wave gets there), so the waves of a SIMD drift apart and one
+    // wave's epilogues overlap the other's MFMAs.
+    int e2_row = -1, e2_it = -1, e2_s = 0, e2_pen = 0;
+    // lower bounds of the tile awaiting epilogue 2 (pass masks of an ambiguous row), as bf16 pairs
+    // rounded toward -inf: a rounded-down lower bound can only add candidates to an ambiguous row's
+    // re-score list, never drop one, and the pair packing keeps the deferral within the registers
+#if RQ_LBF16
+    uint32_t lbp[8];
+#pragma unroll
+    for (int v = 0; v < 8; ++v) lbp[v] = 0u;
+#else
+    float lbf[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) lbf[v] = 0.f;
+#endif
+    auto bf16_down = [](float x) __attribute__((always_inline)) {  // bf16 bits <= x (x finite or inf)
+      const uint32_t u = __float_as_uint(x);
+      return (int32_t)u >= 0 ? (u >> 16) : ((u + 0xFFFFu) >> 16);
+    };
+    auto epilogue2 = [&]() __attribute__((always_inline)) {
+      const int t = e2_it;
+      lds_wait_all<kCW>(ctr_posted, (uint32_t)(t + 1), dead);  // every wave's summary of that tile
+      RS_MARK(5);
+      const float* ex = reinterpret_cast<const float*>(exch + ((t % L::kNE) * kRT + n) * L::kEX);
+      const int2* id_row = reinterpret_cast<const int2*>(smem + L::kIds) + ((t % L::kNE) * kRT + n) * L::kEX;
+      float U = INFINITY;
+#pragma unroll
+      for (int w = 0; w < kCW; ++w) U = fminf(U, ex[4 * w + 2]);
+      // pass: lb < Up, Up above U by >= 2 ulp (a candidate admitted by rounding is only re-scored)
+      const float Up = fmaf(fabsf(U), 0x1p-22f, U) + 1.2e-38f;
+      int cnt = 0, win = 0;
+      bool many = false;
+#pragma unroll
+      for (int w = 0; w < kCW; ++w) {
+        if ((w & 1) == 0) __builtin_amdgcn_sched_barrier(0);
+        const float2 e = *reinterpret_cast<const float2*>(ex + 4 * w);  // {lb of the wave's best, least other lb}
+        const bool pk = (__float_as_uint(e.x - Up) >> 31) != 0;
+        cnt += pk ? 1 : 0;
+        win = pk ? w : win;
+        many = many || (__float_as_uint(e.y - Up) >> 31) != 0;
+      }
+      const int row_id = e2_row;
+      const bool valid = row_id >= 0;
+      const bool definitive = !e2_pen && !many && cnt == 1;
+      // ambiguous rows (a few per cent): every wave's pass-mask word of the row into the LDS mask
+      // buffer (behind a wave-uniform branch: the common tile skips it)
+      const bool amb = valid && !definitive;
+      uint32_t* const mrow = reinterpret_cast<uint32_t*>(smem + L::kMask) + ((t & 1) * kRT + n) * kCW;
+      if (__builtin_amdgcn_ballot_w64(amb)) {
+        uint32_t mk = 0;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+#if RQ_LBF16
+          const float lb = __uint_as_float((v & 1) ? (lbp[v >> 1] & 0xFFFF0000u) : (lbp[v >> 1] << 16));
+#else
+          const float lb = lbf[v];
+#endif
+          mk |= (__float_as_uint(lb - Up) >> 31) << ((v & 3) + 8 * (v >> 2) + 4 * h);
+        }
+        mk |= __shfl_xor(mk, 32);
+        if (h == 0) mrow[cw] = mk;
+      }
+      // All of the tile's global stores come from one wave (rotating), each a single instruction over
+      // the tile's rows: the IDs of definitive rows (the winner's ids from the exchange), the sentinel
+      // -2 and segment of ambiguous rows, and the previous tile's ambiguous rows' pass masks as whole
+      // 32-B work records (complete: every wave has posted this tile, so finished the last epilogue 2).
+      if (cw == (t & (kCW - 1))) {
+        store_masks(prev_row, prev_amb, (t + 1) & 1);
+        if (h == 0 && valid) {
+          if (definitive) {
+            const int2 id = id_row[win];
+            p.out_local[row_id] = id.y;
+            p.out_global[row_id] = id.x;
+          } else {
+            p.out_global[row_id] = -2;
+            seg_of_row[row_id] = e2_pen ? ~e2_s : e2_s;
+          }
+        }
+      }
+      prev_row = row_id;
+      prev_amb = amb;
+      RS_MARK(6);
+    };
     for (int j = tb; j < te; ++j) {
       const int it = j - tb;
       const int b = it & 1;
-      lds_wait_ge(ctr_ready, (uint32_t)(kPW * (it + 1)), dead);  // tile j's image, statistics, info, metadata
+      lds_wait_all<kPW>(ctr_ready, (uint32_t)(it + 1), dead);  // tile j's image, statistics, info, metadata
       const TileInfo ti = read_info(j);
       RS_MARK(1);
       f32x16 acc = {};
@@ -574,7 +693,7 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc, 0, 0, 0);
         }
       }
-      lds_signal(ctr_consumed, lane);  // (the fragment reads are complete: the MFMAs consumed them)
+      lds_publish(ctr_consumed + cw, (uint32_t)(it + 1));  // (fragment reads complete: the MFMAs consumed them)
       RS_MARK(2);
       // the next tile's segment: reload the centres (completed inside: hipcc's wait counting is
       // path-insensitive, a load left pending here would put a wait before every MFMA)
@@ -583,18 +702,17 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
         if (tn.s != ti.s && tn.cnt > 0) load_centres(tn.cnt, tn.cbase);
       }
       RS_MARK(3);
+      if (RQ_DEFER && it > 0) epilogue2();  // tile j-1
       // ---- epilogue 1: per-candidate bounds, this wave's row summary (the collapsed bound of assign.hip)
-      int row_id, my_cid, my_clid;
-      float lbv[16];  // lower bounds, kept for the pass masks of an ambiguous row
-#ifdef RQ_AB_NOEXR
-      float e1U = 0.f, e1lb = 0.f, e1Lo = 0.f;
-#endif
-      float4* const ex_row = exch + ((it & (L::kNE - 1)) * kRT + n) * L::kEX;
-      int2* const id_row = reinterpret_cast<int2*>(smem + L::kIds) + ((it & (L::kNE - 1)) * kRT + n) * L::kEX;
       {
+        float4* const ex_row = exch + ((it % L::kNE) * kRT + n) * L::kEX;
+        int2* const id_row = reinterpret_cast<int2*>(smem + L::kIds) + ((it % L::kNE) * kRT + n) * L::kEX;
         const float4 st = reinterpret_cast<const float4*>(smem + L::kStat)[(it & (L::kNS - 1)) * kRT + n];
         const float m2 = st.x, A2 = st.y;
-        row_id = __float_as_int(st.z);
+        e2_row = __float_as_int(st.z);
+        e2_it = it;
+        e2_s = ti.s;
+        e2_pen = ti.pen;
         const float* csq = csq_base + ti.slot * kNC + 32 * cw + 4 * h;
         const float* cy = cy_base + ti.slot * kNC + 32 * cw + 4 * h;
         float U = INFINITY, lbk = INFINITY, Lo = INFINITY;
@@ -605,6 +723,7 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
           const float2 cs = *reinterpret_cast<const float2*>(csq + 8 * (g >> 1) + 2 * (g & 1));
           const float2 yy = *reinterpret_cast<const float2*>(cy + 8 * (g >> 1) + 2 * (g & 1));
           const float csv[2] = {cs.x, cs.y}, yv[2] = {yy.x, yy.y};
+          uint32_t lbh[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             const int v = 2 * g + e;
@@ -616,8 +735,14 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
             lbk = nm ? lb : lbk;
             kv = nm ? v : kv;
             U = nm ? ub : U;
-            lbv[v] = lb;
+            lbh[e] = bf16_down(lb);
+#if !RQ_LBF16
+            lbf[v] = lb;
+#endif
           }
+#if RQ_LBF16
+          lbp[g] = lbh[0] | (lbh[1] << 16);
+#endif
         }
         // combine the two lane halves of the row (16 candidates each)
         int kpos = 32 * cw + (kv & 3) + 8 * (kv >> 2) + 4 * h;
@@ -629,101 +754,20 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
         kpos = take ? ok : kpos;
         U = take ? oU : U;
         if (h == 0) ex_row[cw] = make_float4(lbk, Lo, U, 0.f);  // (lbk, Lo): an 8-B aligned pair
-#ifdef RQ_AB_NOEXR
-        e1U = U;
-        e1lb = lbk;
-        e1Lo = Lo;
-#endif
         // this wave's candidate ids, posted beside the summary for the tile's store wave
-        my_cid = cid_base[ti.slot * kNC + kpos];
-        my_clid = clid_base[ti.slot * kNC + kpos];
-        if (h == 0) id_row[cw] = make_int2(my_cid, my_clid);
+        if (h == 0) id_row[cw] = make_int2(cid_base[ti.slot * kNC + kpos], clid_base[ti.slot * kNC + kpos]);
       }
-      lds_signal(ctr_posted, lane);
+      lds_publish(ctr_posted + cw, (uint32_t)(it + 1));
       RS_MARK(4);
-#ifndef RQ_AB_NOPOSTWAIT
-      lds_wait_ge(ctr_posted, (uint32_t)(kCW * (it + 1)), dead);  // every wave's summary of tile j
-#endif
-      RS_MARK(5);
-      // ---- epilogue 2: the row decision (every candidate wave computes it for its pass masks)
-#ifndef RQ_AB_NOE2  // (timing-only A/B switches: results wrong)
-      {
-#ifdef RQ_AB_NOEXR
-        float exr[4 * kCW];
-#pragma unroll
-        for (int w = 0; w < 4 * kCW; ++w) exr[w] = (w & 3) == 2 ? e1U : (w & 3) == 0 ? e1lb : e1Lo;
-        const float* ex = exr;
-#else
-        const float* ex = reinterpret_cast<const float*>(ex_row);
-#endif
-        float U = INFINITY;
-#pragma unroll
-        for (int w = 0; w < kCW; ++w) U = fminf(U, ex[4 * w + 2]);
-        // pass: lb < Up, Up above U by >= 2 ulp (a candidate admitted by rounding is only re-scored)
-        const float Up = fmaf(fabsf(U), 0x1p-22f, U) + 1.2e-38f;
-        int cnt = 0, win = 0;
-        bool many = false;
-#pragma unroll
-        for (int w = 0; w < kCW; ++w) {
-          if ((w & 1) == 0) __builtin_amdgcn_sched_barrier(0);
-          const float2 e = *reinterpret_cast<const float2*>(ex + 4 * w);  // {lb of the wave's best, least other lb}
-          const bool pk = (__float_as_uint(e.x - Up) >> 31) != 0;
-          cnt += pk ? 1 : 0;
-          win = pk ? w : win;
-          many = many || (__float_as_uint(e.y - Up) >> 31) != 0;
-        }
-        const bool valid = row_id >= 0;
-        const bool definitive = !ti.pen && !many && cnt == 1;
-        // ambiguous rows (a few per cent): every wave's pass-mask word of the row into the LDS mask
-        // buffer (behind a wave-uniform branch: the common tile skips it)
-        const bool amb = valid && !definitive;
-        uint32_t* const mrow = reinterpret_cast<uint32_t*>(smem + L::kMask) + ((it & 1) * kRT + n) * kCW;
-        if (__builtin_amdgcn_ballot_w64(amb)) {
-          uint32_t mk = 0;
-#pragma unroll
-          for (int v = 0; v < 16; ++v) mk |= (__float_as_uint(lbv[v] - Up) >> 31) << ((v & 3) + 8 * (v >> 2) + 4 * h);
-          mk |= __shfl_xor(mk, 32);
-          if (h == 0) mrow[cw] = mk;
-        }
-        // All of the tile's global stores come from one wave (rotating), each a single instruction over
-        // the tile's rows: the IDs of definitive rows (the winner's ids from the exchange), the sentinel
-        // -2 and segment of ambiguous rows, and the previous tile's ambiguous rows' pass masks as whole
-        // 32-B work records (complete: every wave has posted this tile, so finished the last epilogue).
-        // Eight waves each storing the rows they won, and eight 4-B pieces per work record, cost the
-        // kernel a third of its time in partial-line writes.
-        if (cw == (it & (kCW - 1))) {
-          store_masks(prev_row, prev_amb, (it + 1) & 1);
-          if (h == 0 && valid) {
-            if (definitive) {
-              const int2 id = id_row[win];
-#ifdef RQ_AB_SEQSTORE  // (timing-only: the IDs to tile-ordered positions)
-              const int64_t q = ((int64_t)j * kRT + n) % p.seg_row_off[p.n_segments];
-              p.out_local[q] = id.y;
-              p.out_global[q] = id.x;
-#else
-              p.out_local[row_id] = id.y;
-              p.out_global[row_id] = id.x;
-#endif
-            } else {
-              p.out_global[row_id] = -2;
-              seg_of_row[row_id] = ti.pen ? ~ti.s : ti.s;
-            }
-          }
-        }
-        prev_row = row_id;
-        prev_amb = amb;
-      }
-#else
-      if (row_id == -7) p.out_local[0] = my_cid + my_clid + (int)lbv[3];
-#endif
-      RS_MARK(6);
+      if (!RQ_DEFER) epilogue2();
     }
+    if (RQ_DEFER) epilogue2();  // the last tile
     // the last tile's ambiguous rows: its mask words are complete once every wave has left its last
     // epilogue
-    lds_signal(ctr_posted, lane);
     const int nt = te - tb;
+    lds_publish(ctr_posted + cw, (uint32_t)(nt + 1));
     if (cw == (nt & (kCW - 1))) {
-      lds_wait_ge(ctr_posted, (uint32_t)(kCW * (nt + 1)), dead);
+      lds_wait_all<kCW>(ctr_posted, (uint32_t)(nt + 1), dead);
       store_masks(prev_row, prev_amb, (nt - 1) & 1);
     }
   }
