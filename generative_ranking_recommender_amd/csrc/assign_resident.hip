@@ -55,6 +55,9 @@ constexpr int kPW = 4;                   // producer waves
 constexpr int kRPW = kRT / kPW;          // rows per producer wave per tile
 constexpr int kThreads = (kCW + kPW) * 64;
 constexpr int kNC = kCW * 32;            // candidate capacity
+#ifndef RQ_E1R
+#define RQ_E1R 8  // rounds of LDS metadata reads in epilogue 1
+#endif
 #ifndef RQ_DEFER
 #define RQ_DEFER 1  // epilogue 2 of tile j-1 after tile j's MFMAs
 #endif
@@ -718,8 +721,8 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
         float U = INFINITY, lbk = INFINITY, Lo = INFINITY;
         int kv = 0;
 #pragma unroll
-        for (int g = 0; g < 8; ++g) {  // two candidates at a time (register pressure)
-          __builtin_amdgcn_sched_barrier(0);
+        for (int g = 0; g < 8; ++g) {  // metadata read in RQ_E1R rounds (latency vs register pressure)
+          if (g % (8 / RQ_E1R) == 0) __builtin_amdgcn_sched_barrier(0);
           const float2 cs = *reinterpret_cast<const float2*>(csq + 8 * (g >> 1) + 2 * (g & 1));
           const float2 yy = *reinterpret_cast<const float2*>(cy + 8 * (g >> 1) + 2 * (g & 1));
           const float csv[2] = {cs.x, cs.y}, yv[2] = {yy.x, yy.y};

@@ -15,7 +15,7 @@ from generative_ranking_recommender_amd import _lib, ops  # noqa: E402
 import generative_ranking_recommender_amd.encode as encmod  # noqa: E402
 from generative_ranking_recommender_amd.encode import HIERARCHICAL_TRAIN, RQEncoder  # noqa: E402
 
-PH = {0: {0: "loop", 1: "wait_ready", 2: "mfma", 3: "reload", 4: "epi1", 5: "wait_posted", 6: "epi2"},
+PH = {0: {0: "loop", 1: "wait_ready", 2: "mfma", 3: "reload", 5: "e2_wait_posted", 6: "e2", 4: "epi1"},
       1: {0: "loop", 1: "wait_consumed", 2: "segprep", 3: "produce"}}
 
 
