@@ -16,7 +16,8 @@ PKG = Path(__file__).resolve().parent
 REPO = PKG.parent
 LIB_PATH = PKG / "librqsid.so"
 SRCS = [PKG / "csrc" / "rqsid.hip", PKG / "csrc" / "assign.hip", PKG / "csrc" / "assign_stream.hip",
-        PKG / "csrc" / "assign_resident.hip", PKG / "csrc" / "auction.hip"]
+        PKG / "csrc" / "assign_resident.hip", PKG / "csrc" / "auction.hip",
+        PKG / "csrc" / "auction_seg.hip"]
 DEPS = SRCS + [PKG / "csrc" / "internal.h", PKG / "csrc" / "assign_common.h"]
 HEADER = REPO / "include" / "rqsid.h"
 # host-only I/O library (CSV reader): plain g++, no GPU code
@@ -54,6 +55,12 @@ SIGNATURES = {
     "rqsid_auction_scores": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "rqsid_auction_workspace_bytes": (c_i64, [c_i64, c_i32]),
     "rqsid_auction_lap_half": (c_i32, [c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "rqsid_seg_auction_scores": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp, c_i64, c_i32, c_vp,
+                                         c_vp]),
+    "rqsid_seg_auction_chunk_jobs": (c_i32, []),
+    "rqsid_seg_auction_workspace_bytes": (c_i64, [c_i64, c_i32, c_i32, c_i64, c_i32]),
+    "rqsid_seg_auction_lap_half": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_i32, c_vp,
+                                           c_vp, c_vp, c_i64, c_vp]),
     "rqsid_greedy_match": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "rqsid_mfma_probe": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }

@@ -200,3 +200,96 @@ class KMeans:
         if return_distances:
             return ids, ops.pairwise_distance(X, c)
         return ids
+
+
+def init_indices(num_samples: int, n_clusters: int) -> np.ndarray:
+    """The draw of KMeans.initialize (:240-256): np.random.choice over rows, with replacement only when
+    K > N (global numpy RNG)."""
+    if n_clusters > num_samples:
+        return np.asarray(np.random.choice(num_samples, n_clusters, replace=True))
+    return np.asarray(np.random.choice(num_samples, n_clusters, replace=False))
+
+
+def batched_fit(X: torch.Tensor, layout: "ops.SegmentLayout", n_clusters: int, iter_limits, inits,
+                target_nodes_num=None, tol: float = 1e-3, half: bool = False, balanced: bool = True):
+    """Many independent K-Means fits advanced in lockstep, one per segment of the segment-ordered rows X
+    (segment s = rows layout.off[s] .. layout.off[s+1]), each exactly the iteration of KMeans.fit
+    (:368-465; ``target_nodes_num`` None) or KMeans.fit_by_min_loss (:259-365; re-initialised every 10
+    iterations, keeping the centres of the smallest overflow loss, the latest of equal losses).
+
+    The reference runs these fits one after another (hierarchical_rq_kmeans.py:703-725, 1010-1019); here
+    every iteration of every live segment is one segmented score kernel, one segmented auction
+    (rqsid_seg_auction_lap_half, all rounds of all segments in lockstep) and one centroid update over
+    S*K clusters.  A segment stops at its own iteration limit or tolerance and is skipped afterwards.
+
+    ``inits[s]`` holds segment s's initialisation draws (row indices local to the segment): inits[s][0]
+    for the start and inits[s][i] for the re-initialisation at iteration 10*i.  The caller draws them
+    from the global numpy RNG in segment order, so a segment that runs its full iteration budget consumes
+    exactly the reference's draws.  Empty clusters take a random row of their segment from the global
+    torch RNG, drawn in (iteration, segment, cluster) order.
+
+    Returns (centres f32 [S*K, D], last assignment i32 [N] local to each segment)."""
+    dev = X.device
+    S, K = layout.n_seg, n_clusters
+    off = layout.off
+    if X.shape[0] != layout.n:
+        raise ValueError("batched_fit: rows do not match the segment layout")
+    limits = np.asarray(iter_limits, dtype=np.int64).reshape(S)
+    min_loss_mode = target_nodes_num is not None
+
+    def gather(draws, segs):
+        idx = np.concatenate([off[s] + np.asarray(draws[i], dtype=np.int64) for i, s in enumerate(segs)])
+        return X[torch.from_numpy(idx).to(dev)]
+
+    centers = gather([inits[s][0] for s in range(S)], range(S)).float().contiguous()
+    active = layout.sizes > 0
+    iteration = np.zeros(S, dtype=np.int64)
+    min_loss = np.full(S, np.inf)
+    best = centers.clone()
+    last = torch.full((max(layout.n, 1),), -1, dtype=torch.int32, device=dev)
+    seg_row = layout.seg_of_row
+    buckets = cand = None
+    if min_loss_mode or not balanced:
+        buckets = ops.bucket(seg_row, S)
+        cand = ops.contiguous_candidates(S, K, dev)
+    rows_of = torch.arange(S * K, device=dev).view(S, K)
+    while active.any():
+        if min_loss_mode:
+            re = np.nonzero(active & (iteration > 0) & (iteration % 10 == 0))[0]
+            if len(re):
+                centers[rows_of[torch.from_numpy(re).to(dev)].reshape(-1)] = gather(
+                    [inits[s][iteration[s] // 10] for s in re], re).float()
+        act_t = torch.from_numpy(active.astype(np.uint8)).to(dev)
+        if balanced:
+            w = ops.seg_auction_scores(X, centers, K, layout, half=half)
+            a, _ = ops.seg_auction(w, K, layout, act_t, out=last)
+            del w
+        else:
+            a = ops.assign(X, ops.prepare_centers(centers), buckets, cand)[0]
+            keep = ~act_t.bool()[seg_row]
+            a = torch.where(keep, last[:layout.n], a)
+        last[:layout.n] = a
+        prev = centers
+        gid = seg_row * K + a.long()
+        new, counts = ops.centroid_update(X, gid, S * K, centers.clone())
+        cnt = counts.cpu().numpy().reshape(S, K)
+        for s in np.nonzero(active)[0]:
+            for k in np.nonzero(cnt[s] == 0)[0]:
+                new[s * K + k] = X[int(off[s]) + int(torch.randint(int(layout.sizes[s]), (1,)).item())]
+        frozen = torch.from_numpy(~active).to(dev)
+        new[frozen.repeat_interleave(K)] = prev[frozen.repeat_interleave(K)]
+        centers = new.contiguous()
+        shift = torch.sqrt(torch.sum((centers - prev) ** 2, dim=1)).view(S, K).sum(1).cpu().numpy()
+        if min_loss_mode:
+            glob = ops.assign(X, ops.prepare_centers(centers), buckets, cand)[1]
+            hist = torch.bincount(glob.long(), minlength=S * K).view(S, K)
+            loss = (hist - target_nodes_num).clamp(min=0).sum(1).cpu().numpy()
+            better = active & (loss <= min_loss)
+            if better.any():
+                min_loss[better] = loss[better]
+                sel = rows_of[torch.from_numpy(np.nonzero(better)[0]).to(dev)].reshape(-1)
+                best[sel] = centers[sel]
+        iteration[active] += 1
+        done = active & ((shift.astype(np.float64) ** 2 < tol) | ((limits != 0) & (iteration >= limits)))
+        active &= ~done
+    return (best if min_loss_mode else centers), last[:layout.n]

@@ -1,0 +1,657 @@
+// auction_seg.hip — many independent balanced assignments (balancekmeans.auction_lap_half,
+// balancekmeans/__init__.py:12-140) advanced in lockstep: the per-parent sub-K-Means of the middle layer
+// (hierarchical_rq_kmeans.py:671-752) and the per-(l1, l2) group sub-K-Means of the last-layer match
+// matrix (:968-1053) run one auction per segment, and the reference runs them one after another.  Here
+// every round of every live segment is one sequence of launches over all segments (SURVEY.md §7 item 6,
+// hard part 5), and segments finish independently (13 rounds when N_s % K == 0, 1002 otherwise).
+//
+// Segment s: jobs seg_off[s] .. seg_off[s+1] (N_s of them), workers 0 .. K-1, scores at
+// W + K*seg_off[s] as a [K][N_s] worker-major fp16 block.  Inside a segment every step is the
+// single-auction step of auction.hip (same fp16 operations, same tie rule: the lowest job indices are
+// kept at the top-k boundary, equal highest bids go to the lowest worker), so segment s's result is
+// bit-identical to rqsid_auction_lap_half on its block alone.
+//
+// Jobs are cut into chunks of kCh jobs that never straddle segments (seg_chunk_off = exclusive scan of
+// ceil(N_s / kCh)).  A segment of one chunk (the last layer's groups: median ~600 rows) selects its
+// per-worker thresholds inside one block from LDS histograms (sa_small_select_kernel); wider segments
+// (the middle layer's parents) use per-(segment, worker) global histograms like auction.hip.
+#include <cmath>
+
+#include "internal.h"
+
+namespace rqsid {
+namespace {
+
+constexpr int kKG = 16;        // workers per block
+constexpr int kCh = 1024;      // jobs per chunk
+constexpr int kJPT = kCh / 256;
+
+__device__ __forceinline__ float h2f(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+__device__ __forceinline__ uint32_t okey(uint16_t b) {
+  if (b == 0x8000u) b = 0;
+  return (b & 0x8000u) ? (~b & 0xFFFFu) : (b | 0x8000u);
+}
+__device__ __forceinline__ uint16_t okey_inv(uint32_t k) {
+  return (k & 0x8000u) ? (uint16_t)(k & 0x7FFFu) : (uint16_t)(~k & 0xFFFFu);
+}
+
+// seg_flag bits
+constexpr uint8_t kLive = 1;     // segment still bidding
+constexpr uint8_t kSingle = 2;   // one chunk: LDS selection
+
+struct SegAuction {
+  const uint16_t* W;
+  int32_t K;
+  int32_t S;
+  int64_t total_chunks;
+  const int32_t* seg_off;        // [S+1] jobs
+  const int32_t* chunk_off;      // [S+1] chunks
+  uint8_t* flag;                 // [S]
+  uint16_t* eps;                 // [S]
+  uint32_t* mm;                  // [S][2] max key, min key
+  uint32_t* have;                // [S] jobs with a bidder this round
+  int32_t* rounds;               // [S] rounds run (device)
+  uint32_t* live_count;          // [1]
+  uint16_t* cost;                // [N]
+  int32_t* hb;                   // [N]
+  uint8_t* nobid;                // [N]
+  uint32_t* key;                 // [N]
+  int32_t n_multi;               // segments of more than one chunk
+  int32_t* hidx;                 // [S] rank among the multi-chunk segments (-1: one chunk)
+  int32_t* mseg;                 // [n_multi] the multi-chunk segments in order
+  uint32_t* hist;                // [n_multi*K][256]
+  uint32_t* sel;                 // [S*K][4]: b1, rank in bin, T, need_eq
+  uint32_t* eqcnt;               // [K][total_chunks]
+};
+
+__device__ __forceinline__ int seg_of(const int32_t* __restrict__ off, int n_seg, int64_t i) {
+  int lo = 0, hi = n_seg - 1;  // last s with off[s] <= i
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int64_t)off[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+struct ChunkInfo {
+  int s;
+  int64_t seg_j0;   // first job of the segment
+  int64_t n_s;      // jobs in the segment
+  int64_t j0;       // first job of the chunk (global)
+  int64_t nj;       // jobs in the chunk
+  int64_t cis;      // chunk index inside the segment
+};
+
+__device__ __forceinline__ ChunkInfo chunk_info(const SegAuction& a, int64_t c) {
+  ChunkInfo ci;
+  ci.s = seg_of(a.chunk_off, a.S, c);
+  ci.seg_j0 = a.seg_off[ci.s];
+  ci.n_s = a.seg_off[ci.s + 1] - ci.seg_j0;
+  ci.cis = c - a.chunk_off[ci.s];
+  ci.j0 = ci.seg_j0 + ci.cis * kCh;
+  ci.nj = min((int64_t)kCh, ci.seg_j0 + ci.n_s - ci.j0);
+  return ci;
+}
+
+__device__ __forceinline__ uint16_t value_bits(int w, uint16_t wv, int32_t hbj, uint16_t cj) {
+  if (hbj == w) return wv;  // the previous round's winner keeps its raw score
+  return f2h(h2f(wv) - h2f(cj));
+}
+
+__device__ __forceinline__ const uint16_t* wrow(const SegAuction& a, const ChunkInfo& ci, int w) {
+  return a.W + (int64_t)a.K * ci.seg_j0 + (int64_t)w * ci.n_s - ci.seg_j0;  // index with the global job
+}
+
+// ---- setup ----
+__global__ __launch_bounds__(256) void sa_seg_init_kernel(SegAuction a, const uint8_t* __restrict__ active) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= a.S) return;
+  const int64_t n_s = a.seg_off[s + 1] - a.seg_off[s];
+  const int64_t nch = a.chunk_off[s + 1] - a.chunk_off[s];
+  uint8_t f = 0;
+  // live: requested, non-empty, and N_s >= K (N_s < K takes the argmin fallback, 0 rounds)
+  if ((!active || active[s]) && n_s > 0 && n_s >= a.K) f |= kLive;
+  if (nch == 1) f |= kSingle;
+  a.flag[s] = f;
+  a.mm[2 * s] = 0;
+  a.mm[2 * s + 1] = 0xFFFFFFFFu;
+  a.have[s] = 0;
+  a.rounds[s] = 0;
+}
+
+__global__ __launch_bounds__(256) void sa_job_init_kernel(SegAuction a, int64_t n) {
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += (int64_t)gridDim.x * 256) {
+    a.cost[j] = 0;
+    a.hb[j] = -1;
+    a.nobid[j] = 0;
+    a.key[j] = 0;
+  }
+}
+
+// min / max of each live segment's whole score block (eps), one block per (chunk, worker group)
+__global__ __launch_bounds__(256) void sa_minmax_kernel(SegAuction a) {
+  const ChunkInfo ci = chunk_info(a, blockIdx.x);
+  if (!(a.flag[ci.s] & kLive)) return;
+  const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
+  uint32_t mx = 0, mn = 0xFFFFFFFFu;
+  for (int g = 0; g < nw; ++g) {
+    const uint16_t* row = wrow(a, ci, w0 + g);
+    for (int64_t t = threadIdx.x; t < ci.nj; t += 256) {
+      const uint32_t k = okey(row[ci.j0 + t]);
+      mx = max(mx, k);
+      mn = min(mn, k);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(&a.mm[2 * ci.s], mx);
+    atomicMin(&a.mm[2 * ci.s + 1], mn);
+  }
+}
+
+__global__ __launch_bounds__(256) void sa_eps_kernel(SegAuction a) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= a.S || !(a.flag[s] & kLive)) return;
+  const float mx = h2f(okey_inv(a.mm[2 * s])), mn = h2f(okey_inv(a.mm[2 * s + 1]));
+  const uint16_t spread = f2h(mx - mn);
+  uint16_t eps = f2h(h2f(spread) / 50.0f);
+  const uint16_t floor_eps = f2h(1e-4f);
+  if (!(h2f(eps) >= h2f(floor_eps))) eps = floor_eps;
+  a.eps[s] = eps;
+}
+
+// N_s < K: the reference's argmin(-D) fallback (the FARTHEST centre), balancekmeans/__init__.py:24-26
+__global__ __launch_bounds__(256) void sa_fallback_kernel(SegAuction a, int32_t* __restrict__ out) {
+  const ChunkInfo ci = chunk_info(a, blockIdx.x);
+  if (ci.n_s >= a.K || ci.n_s == 0) return;
+  for (int64_t t = threadIdx.x; t < ci.nj; t += 256) {
+    const int64_t j = ci.j0 + t;
+    float best = INFINITY;
+    int bw = 0;
+    for (int w = 0; w < a.K; ++w) {
+      const float v = h2f(wrow(a, ci, w)[j]);
+      if (v < best) { best = v; bw = w; }
+    }
+    out[j] = bw;
+  }
+}
+
+// ---- selection of the (jpw+1)-th largest value per (segment, worker) ----
+// Walk a 256-bin histogram from the top for the bin holding `rank` (1-based): one wave, 4 bins a lane.
+// Returns the bin b and the count strictly above it (b stops at 0 like the serial walk of auction.hip).
+__device__ __forceinline__ void wave_select(const uint32_t* __restrict__ h, uint32_t rank, uint32_t& bin,
+                                            uint32_t& above) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t h0 = h[4 * lane], h1 = h[4 * lane + 1], h2 = h[4 * lane + 2], h3 = h[4 * lane + 3];
+  const uint32_t own = h0 + h1 + h2 + h3;
+  uint32_t suf = own;  // inclusive suffix sum over lanes >= lane
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_down((int)suf, o);
+    if (lane + o < 64) suf += y;
+  }
+  const unsigned long long m = __ballot(suf >= rank);
+  const int L = m ? 63 - __clzll(m) : 0;
+  uint32_t b = 0, ab = 0;
+  if (lane == L) {
+    uint32_t acc = suf - own;  // strictly above this lane's bins
+    const uint32_t hv[4] = {h0, h1, h2, h3};
+    int q = 3;
+    for (; q > 0; --q) {
+      if (acc + hv[q] >= rank) break;
+      acc += hv[q];
+    }
+    // lane 0 bin 0 is the floor; a higher lane's bin 4L may still fall through to a lower lane only if
+    // the ballot was empty, which cannot happen while the segment holds >= rank values
+    b = 4 * L + q;
+    ab = acc;
+  }
+  bin = (uint32_t)__shfl((int)b, L);
+  above = (uint32_t)__shfl((int)ab, L);
+}
+
+// multi-chunk segments: global histograms
+template <bool LOW>
+__global__ __launch_bounds__(256) void sa_hist_kernel(SegAuction a) {
+  const ChunkInfo ci = chunk_info(a, blockIdx.x);
+  const uint8_t f = a.flag[ci.s];
+  if (!(f & kLive) || (f & kSingle)) return;
+  __shared__ uint32_t h[kKG][256];
+  const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
+  for (int i = threadIdx.x; i < kKG * 256; i += 256) (&h[0][0])[i] = 0;
+  __syncthreads();
+  const int64_t sw0 = (int64_t)ci.s * a.K + w0;
+  const int64_t hw0 = (int64_t)a.hidx[ci.s] * a.K + w0;
+  uint32_t b1[kKG];
+  if (LOW)
+    for (int g = 0; g < kKG; ++g) b1[g] = g < nw ? a.sel[(sw0 + g) * 4 + 0] : 0;
+  for (int t = 0; t < kJPT; ++t) {
+    const int64_t jj = t * 256 + threadIdx.x;
+    if (jj >= ci.nj) break;
+    const int64_t j = ci.j0 + jj;
+    const int32_t hbj = a.hb[j];
+    const uint16_t cj = a.cost[j];
+    for (int g = 0; g < nw; ++g) {
+      const uint32_t k = okey(value_bits(w0 + g, wrow(a, ci, w0 + g)[j], hbj, cj));
+      if (!LOW) atomicAdd(&h[g][k >> 8], 1u);
+      else if ((k >> 8) == b1[g]) atomicAdd(&h[g][k & 255], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nw * 256; i += 256) {
+    const uint32_t c = (&h[0][0])[i];
+    if (c) atomicAdd(&a.hist[(hw0 + i / 256) * 256 + (i & 255)], c);
+  }
+}
+
+// one wave per (segment, worker) of the multi-chunk segments
+template <bool LOW>
+__global__ __launch_bounds__(256) void sa_select_kernel(SegAuction a) {
+  const int64_t hw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (hw >= (int64_t)a.n_multi * a.K) return;
+  const int s = a.mseg[hw / a.K];
+  const int w = (int)(hw % a.K);
+  if (!(a.flag[s] & kLive)) return;
+  const int64_t n_s = a.seg_off[s + 1] - a.seg_off[s];
+  const uint32_t jpw = (uint32_t)(n_s / a.K);
+  uint32_t* h = a.hist + hw * 256;
+  uint32_t* sel = a.sel + ((int64_t)s * a.K + w) * 4;
+  const uint32_t rank = LOW ? sel[1] : jpw + 1;
+  uint32_t b, above;
+  wave_select(h, rank, b, above);
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) {
+    if (!LOW) {
+      sel[0] = b;
+      sel[1] = rank - above;
+      sel[3] = above;
+    } else {
+      const uint32_t T = (sel[0] << 8) | b;
+      const uint32_t c_gt = sel[3] + above;
+      sel[2] = T;
+      sel[3] = jpw - c_gt;
+    }
+  }
+  for (int i = lane; i < 256; i += 64) h[i] = 0;  // ready for the next histogram
+}
+
+// one-chunk segments: both histogram passes and both selections inside the block; the chunk offset of
+// the tie ranks is 0
+__global__ __launch_bounds__(256) void sa_small_select_kernel(SegAuction a) {
+  const ChunkInfo ci = chunk_info(a, blockIdx.x);
+  const uint8_t f = a.flag[ci.s];
+  if (!(f & kLive) || !(f & kSingle)) return;
+  __shared__ uint32_t h[kKG][256];
+  __shared__ uint32_t b1s[kKG], rk[kKG], ab1[kKG];
+  const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
+  const int64_t sw0 = (int64_t)ci.s * a.K + w0;
+  const uint32_t jpw = (uint32_t)(ci.n_s / a.K);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int i = threadIdx.x; i < kKG * 256; i += 256) (&h[0][0])[i] = 0;
+    __syncthreads();
+    for (int t = 0; t < kJPT; ++t) {
+      const int64_t jj = t * 256 + threadIdx.x;
+      if (jj >= ci.nj) break;
+      const int64_t j = ci.j0 + jj;
+      const int32_t hbj = a.hb[j];
+      const uint16_t cj = a.cost[j];
+      for (int g = 0; g < nw; ++g) {
+        const uint32_t k = okey(value_bits(w0 + g, wrow(a, ci, w0 + g)[j], hbj, cj));
+        if (pass == 0) atomicAdd(&h[g][k >> 8], 1u);
+        else if ((k >> 8) == b1s[g]) atomicAdd(&h[g][k & 255], 1u);
+      }
+    }
+    __syncthreads();
+    for (int g = wv; g < nw; g += 4) {
+      uint32_t b, above;
+      const uint32_t rank = pass == 0 ? jpw + 1 : rk[g];
+      wave_select(h[g], rank, b, above);
+      if (lane == 0) {
+        if (pass == 0) {
+          b1s[g] = b;
+          rk[g] = rank - above;
+          ab1[g] = above;
+        } else {
+          uint32_t* sel = a.sel + (sw0 + g) * 4;
+          const uint32_t T = (b1s[g] << 8) | b;
+          sel[0] = b1s[g];
+          sel[2] = T;
+          sel[3] = jpw - (ab1[g] + above);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- tie counts (multi-chunk segments) ----
+__global__ __launch_bounds__(256) void sa_eqcount_kernel(SegAuction a) {
+  const ChunkInfo ci = chunk_info(a, blockIdx.x);
+  const uint8_t f = a.flag[ci.s];
+  if (!(f & kLive) || (f & kSingle)) return;
+  __shared__ uint32_t c[kKG];
+  const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
+  const int64_t sw0 = (int64_t)ci.s * a.K + w0;
+  if (threadIdx.x < kKG) c[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t T[kKG];
+  for (int g = 0; g < kKG; ++g) T[g] = g < nw ? a.sel[(sw0 + g) * 4 + 2] : 0xFFFFFFFFu;
+  uint32_t cnt[kKG] = {};
+  for (int t = 0; t < kJPT; ++t) {
+    const int64_t jj = t * 256 + threadIdx.x;
+    if (jj >= ci.nj) break;
+    const int64_t j = ci.j0 + jj;
+    const int32_t hbj = a.hb[j];
+    const uint16_t cj = a.cost[j];
+    for (int g = 0; g < nw; ++g) cnt[g] += okey(value_bits(w0 + g, wrow(a, ci, w0 + g)[j], hbj, cj)) == T[g];
+  }
+  for (int g = 0; g < nw; ++g) {
+    uint32_t v = cnt[g];
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&c[g], v);
+  }
+  __syncthreads();
+  if (threadIdx.x < nw) a.eqcnt[(int64_t)(w0 + threadIdx.x) * a.total_chunks + blockIdx.x] = c[threadIdx.x];
+}
+
+// exclusive scan of the tie counts over a segment's chunks: one wave per (segment, worker)
+__global__ __launch_bounds__(256) void sa_eqscan_kernel(SegAuction a) {
+  const int64_t hw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (hw >= (int64_t)a.n_multi * a.K) return;
+  const int s = a.mseg[hw / a.K];
+  const int w = (int)(hw % a.K);
+  if (!(a.flag[s] & kLive)) return;
+  const int lane = threadIdx.x & 63;
+  uint32_t* e = a.eqcnt + (int64_t)w * a.total_chunks;
+  const int64_t c0 = a.chunk_off[s], c1 = a.chunk_off[s + 1];
+  uint32_t carry = 0;
+  for (int64_t base = c0; base < c1; base += 64) {
+    const int64_t i = base + lane;
+    const uint32_t v = i < c1 ? e[i] : 0;
+    uint32_t x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+      if (lane >= o) x += y;
+    }
+    if (i < c1) e[i] = carry + x - v;
+    carry += (uint32_t)__shfl((int)x, 63);
+  }
+}
+
+// ---- bids: one packed {fp16 bid, ~worker} atomicMax per job and block ----
+__global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a, int counter) {
+  const ChunkInfo ci = chunk_info(a, blockIdx.x);
+  const uint8_t f = a.flag[ci.s];
+  if (!(f & kLive)) return;
+  __shared__ uint32_t wsum[kKG][4];
+  const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
+  const int64_t sw0 = (int64_t)ci.s * a.K + w0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint16_t eps = a.eps[ci.s];
+  const float epsf = h2f(eps);
+  uint32_t T[kKG], need[kKG], off[kKG];
+  float vT[kKG];
+  for (int g = 0; g < kKG; ++g) {
+    T[g] = g < nw ? a.sel[(sw0 + g) * 4 + 2] : 0xFFFFFFFFu;
+    need[g] = g < nw ? a.sel[(sw0 + g) * 4 + 3] : 0;
+    off[g] = (g < nw && !(f & kSingle)) ? a.eqcnt[(int64_t)(w0 + g) * a.total_chunks + blockIdx.x] : 0;
+    vT[g] = g < nw ? h2f(okey_inv(T[g])) : 0.f;
+  }
+  for (int t = 0; t < kJPT; ++t) {
+    const int64_t jj = t * 256 + threadIdx.x;
+    const bool live = jj < ci.nj;
+    const int64_t j = ci.j0 + jj;
+    const int32_t hbj = live ? a.hb[j] : -1;
+    const uint16_t cj = live ? a.cost[j] : 0;
+    const bool nob = live && a.nobid[j];
+    uint32_t best = 0;
+    for (int g = 0; g < nw; ++g) {
+      const int w = w0 + g;
+      const uint16_t vb = live ? value_bits(w, wrow(a, ci, w)[j], hbj, cj) : 0;
+      const uint32_t k = okey(vb);
+      const bool eq = live && k == T[g];
+      const unsigned long long m = __ballot(eq);
+      const uint32_t before_in_wave = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == 0) wsum[g][wv] = __popcll(m);
+      __syncthreads();
+      uint32_t before = off[g] + before_in_wave;
+      for (int q = 0; q < wv; ++q) before += wsum[g][q];
+      const uint32_t tot = wsum[g][0] + wsum[g][1] + wsum[g][2] + wsum[g][3];
+      __syncthreads();
+      off[g] += tot;
+      uint16_t bid = 0;
+      if (live && k > T[g]) {
+        bid = f2h(h2f(f2h(h2f(vb) - vT[g])) + epsf);
+      } else if (eq && before < need[g]) {
+        bid = f2h(0.0f + epsf);
+      }
+      if (counter < 100 && hbj == w) bid = eps;        // retention bid of the previous winner
+      if (counter > 1000 && w == 0 && nob) bid = eps;  // leftovers go to worker 0
+      if (bid) best = max(best, ((uint32_t)bid << 16) | (0xFFFFu - (uint32_t)w));
+    }
+    if (best) atomicMax(&a.key[j], best);
+  }
+}
+
+// ---- resolve: per job of the live segments, one block per chunk ----
+__global__ __launch_bounds__(256) void sa_resolve_kernel(SegAuction a, int32_t* __restrict__ out) {
+  const ChunkInfo ci = chunk_info(a, blockIdx.x);
+  if (!(a.flag[ci.s] & kLive)) return;
+  uint32_t cnt = 0;
+  for (int64_t t = threadIdx.x; t < ci.nj; t += 256) {
+    const int64_t j = ci.j0 + t;
+    const uint32_t k = a.key[j];
+    a.key[j] = 0;
+    if (k) {
+      const int32_t w = (int32_t)(0xFFFFu - (k & 0xFFFFu));
+      const uint16_t bid = (uint16_t)(k >> 16);
+      out[j] = w;
+      a.hb[j] = w;
+      a.nobid[j] = 0;
+      a.cost[j] = f2h(h2f(a.cost[j]) + h2f(bid));
+      ++cnt;
+    } else {
+      out[j] = -1;
+      a.hb[j] = -1;
+      a.nobid[j] = 1;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&a.have[ci.s], cnt);
+}
+
+// end of round r: a segment whose every job has a bidder is done after r+1 rounds
+__global__ __launch_bounds__(256) void sa_round_end_kernel(SegAuction a, int round, int count) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  uint32_t live = 0;
+  if (s < a.S && (a.flag[s] & kLive)) {
+    const int64_t n_s = a.seg_off[s + 1] - a.seg_off[s];
+    a.rounds[s] = round + 1;
+    if ((int64_t)a.have[s] == n_s) a.flag[s] &= ~kLive;
+    else live = 1;
+    a.have[s] = 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) live += (uint32_t)__shfl_xor((int)live, o);
+  if (count && (threadIdx.x & 63) == 0 && live) atomicAdd(a.live_count, live);
+}
+
+// multi-chunk segment ranks (one block): hidx[s] = rank or -1, mseg[rank] = s; live_count[1] = total
+__global__ __launch_bounds__(1024) void sa_multi_index_kernel(SegAuction a) {
+  __shared__ uint32_t ws[16];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int base = 0; base < a.S; base += 1024) {
+    const int s = base + threadIdx.x;
+    const uint32_t v = (s < a.S && a.chunk_off[s + 1] - a.chunk_off[s] > 1) ? 1u : 0u;
+    const unsigned long long m = __ballot(v);
+    const uint32_t before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) ws[wv] = __popcll(m);
+    __syncthreads();
+    uint32_t off = carry;
+    for (int q = 0; q < wv; ++q) off += ws[q];
+    if (s < a.S) {
+      const uint32_t r = off + before;
+      a.hidx[s] = v ? (int32_t)r : -1;
+      if (v && (int32_t)r < a.n_multi) a.mseg[r] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int q = 0; q < 16; ++q) t += ws[q];
+      carry += t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.live_count[1] = carry;
+}
+
+struct Carve {
+  char* p;
+  int64_t used = 0;
+  template <class T>
+  T* take(int64_t n) {
+    T* r = reinterpret_cast<T*>(p + used);
+    used += (n * (int64_t)sizeof(T) + 255) / 256 * 256;
+    return r;
+  }
+};
+
+// workspace layout (also the size query when p == nullptr)
+void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t total_chunks) {
+  a.flag = c.take<uint8_t>(S);
+  a.eps = c.take<uint16_t>(S);
+  a.mm = c.take<uint32_t>(2 * (int64_t)S);
+  a.have = c.take<uint32_t>(S);
+  a.live_count = c.take<uint32_t>(2);
+  a.hidx = c.take<int32_t>(S);
+  a.mseg = c.take<int32_t>(a.n_multi > 0 ? a.n_multi : 1);
+  a.cost = c.take<uint16_t>(N);
+  a.hb = c.take<int32_t>(N);
+  a.nobid = c.take<uint8_t>(N);
+  a.key = c.take<uint32_t>(N);
+  a.hist = c.take<uint32_t>((int64_t)a.n_multi * K * 256);
+  a.sel = c.take<uint32_t>((int64_t)S * K * 4);
+  a.eqcnt = c.take<uint32_t>((int64_t)K * total_chunks);
+}
+
+}  // namespace
+}  // namespace rqsid
+
+using namespace rqsid;
+
+extern "C" {
+
+int32_t rqsid_seg_auction_chunk_jobs(void) { return kCh; }
+
+int64_t rqsid_seg_auction_workspace_bytes(int64_t n_jobs, int32_t n_workers, int32_t n_seg, int64_t total_chunks,
+                                          int32_t n_multi) {
+  if (n_jobs < 0 || n_workers <= 0 || n_seg <= 0 || total_chunks < 0 || n_multi < 0 || n_multi > n_seg) return -1;
+  SegAuction a{};
+  a.n_multi = n_multi;
+  Carve c{nullptr};
+  carve(a, c, n_jobs, n_workers, n_seg, total_chunks);
+  return c.used;
+}
+
+int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_t n_seg, const int32_t* seg_off,
+                               const int32_t* seg_chunk_off, int64_t total_chunks, int32_t n_multi, int64_t n_jobs,
+                               const uint8_t* active, int32_t max_rounds, int32_t* out_assign, int32_t* out_rounds,
+                               void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!scores || !seg_off || !seg_chunk_off || !out_assign || !out_rounds || n_workers <= 0 || n_seg <= 0 ||
+      total_chunks < 0 || total_chunks > INT32_MAX || n_jobs < 0 || n_jobs > INT32_MAX || n_multi < 0 ||
+      n_multi > n_seg)
+    return fail(RQSID_E_ARG, "seg_auction: bad arguments (K=%d S=%d chunks=%lld multi=%d)", n_workers, n_seg,
+                (long long)total_chunks, n_multi);
+  if (n_workers == 1) return fail(RQSID_E_ARG, "seg_auction: a single worker cannot bid on N + 1 jobs");
+  if (!workspace ||
+      workspace_bytes < rqsid_seg_auction_workspace_bytes(n_jobs, n_workers, n_seg, total_chunks, n_multi))
+    return fail(RQSID_E_WORKSPACE, "seg_auction: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  SegAuction a{};
+  a.W = scores;
+  a.K = n_workers;
+  a.S = n_seg;
+  a.total_chunks = total_chunks;
+  a.seg_off = seg_off;
+  a.chunk_off = seg_chunk_off;
+  a.rounds = out_rounds;
+  a.n_multi = n_multi;
+  Carve c{(char*)workspace};
+  carve(a, c, n_jobs, n_workers, n_seg, total_chunks);
+  const unsigned gs = (unsigned)cdiv(n_seg, 256);
+  uint32_t* host = nullptr;  // pinned readback: [0] live segments, [1] multi-chunk segments
+  if (hipHostMalloc((void**)&host, 2 * sizeof(uint32_t)) != hipSuccess)
+    return fail(RQSID_E_LAUNCH, "seg_auction: pinned readback buffer");
+  int rc = RQSID_OK;
+  hipLaunchKernelGGL(sa_seg_init_kernel, dim3(gs), dim3(256), 0, st, a, active);
+  hipLaunchKernelGGL(sa_multi_index_kernel, dim3(1), dim3(1024), 0, st, a);
+  if ((rc = check_launch("seg_auction_init")) ||
+      hipMemcpyAsync(host, a.live_count, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    (void)hipHostFree(host);
+    return rc ? rc : fail(RQSID_E_LAUNCH, "seg_auction: init readback");
+  }
+  if ((int32_t)host[1] != n_multi) {
+    (void)hipHostFree(host);
+    return fail(RQSID_E_ARG, "seg_auction: %u segments span more than one chunk, n_multi = %d", host[1], n_multi);
+  }
+  if (total_chunks == 0) {
+    (void)hipHostFree(host);
+    return RQSID_OK;
+  }
+  const bool any_single = n_multi < n_seg;
+  if (n_multi > 0 && hipMemsetAsync(a.hist, 0, (size_t)n_multi * n_workers * 256 * 4, st) != hipSuccess) {
+    (void)hipHostFree(host);
+    return fail(RQSID_E_LAUNCH, "seg_auction: memset");
+  }
+  hipLaunchKernelGGL(sa_job_init_kernel, dim3(grid_cap(cdiv(n_jobs, 256), 8192)), dim3(256), 0, st, a, n_jobs);
+  const dim3 gcw((unsigned)total_chunks, (unsigned)cdiv(n_workers, kKG));
+  const dim3 gc((unsigned)total_chunks);
+  const unsigned gmw = (unsigned)cdiv((int64_t)n_multi * n_workers, 4);
+  hipLaunchKernelGGL(sa_fallback_kernel, gc, dim3(256), 0, st, a, out_assign);
+  hipLaunchKernelGGL(sa_minmax_kernel, gcw, dim3(256), 0, st, a);
+  hipLaunchKernelGGL(sa_eps_kernel, dim3(gs), dim3(256), 0, st, a);
+  if ((rc = check_launch("seg_auction_init"))) {
+    (void)hipHostFree(host);
+    return rc;
+  }
+  // The live count is read back every kPoll rounds (rounds of finished segments are no-ops, so polling
+  // late only costs a few empty launches); only the polled round counts, into a zeroed counter.
+  constexpr int kPoll = 8;
+  if (hipMemsetAsync(a.live_count, 0, 4, st) != hipSuccess) rc = fail(RQSID_E_LAUNCH, "seg_auction: memset");
+  for (int round = 0; rc == RQSID_OK && (max_rounds <= 0 || round < max_rounds); ++round) {
+    if (n_multi > 0) {
+      hipLaunchKernelGGL((sa_hist_kernel<false>), gcw, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((sa_select_kernel<false>), dim3(gmw), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((sa_hist_kernel<true>), gcw, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((sa_select_kernel<true>), dim3(gmw), dim3(256), 0, st, a);
+      hipLaunchKernelGGL(sa_eqcount_kernel, gcw, dim3(256), 0, st, a);
+      hipLaunchKernelGGL(sa_eqscan_kernel, dim3(gmw), dim3(256), 0, st, a);
+    }
+    if (any_single) hipLaunchKernelGGL(sa_small_select_kernel, gcw, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(sa_bid_kernel, gcw, dim3(256), 0, st, a, round);
+    hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, st, a, out_assign);
+    const bool last = max_rounds > 0 && round + 1 >= max_rounds;
+    const bool poll = (round + 1) % kPoll == 0 || last;
+    hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, st, a, round, (int)poll);
+    if ((rc = check_launch("seg_auction_round"))) break;
+    if (!poll) continue;
+    if (hipMemcpyAsync(host, a.live_count, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemsetAsync(a.live_count, 0, 4, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+      rc = fail(RQSID_E_LAUNCH, "seg_auction: readback");
+      break;
+    }
+    if (host[0] == 0) break;
+    if (last) rc = fail(RQSID_E_LAUNCH, "seg_auction: %u segments still bidding after %d rounds", host[0], max_rounds);
+  }
+  (void)hipHostFree(host);
+  return rc;
+}
+
+}  // extern "C"

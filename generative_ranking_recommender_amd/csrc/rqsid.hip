@@ -320,15 +320,42 @@ constexpr int kPdTile = 64;
 // MODE 1: out16[k][n] = fp16(-distance): the auction's worker-major score matrix (auction_lap_half(-D), :29-43)
 // MODE 2: as 1 from fp16-rounded operands with the distance rounded to fp16 and clamped at 1e-5
 //         (pairwise_distance_half, :536-574)
-template <int MODE>
+//
+// SEG (modes 1/2 only): segment s owns rows seg_off[s]..seg_off[s+1] and centres s*k .. s*k+k-1; its
+// scores go to out16 + k*seg_off[s] as a [k][n_s] worker-major block (the segmented auction's layout).
+// Row tiles never straddle segments: blockIdx.x indexes the tile list seg_tile_off (exclusive scan of
+// ceil(n_s / 64)).  The arithmetic is the unsegmented kernel's, so each block equals a per-segment call.
+__device__ __forceinline__ int seg_of(const int32_t* __restrict__ off, int n_seg, int64_t i) {
+  int lo = 0, hi = n_seg - 1;  // last s with off[s] <= i
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((int64_t)off[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+template <int MODE, bool SEG = false>
 __global__ __launch_bounds__(256) void pairwise_distance_kernel(const float* __restrict__ x, int64_t n, int dim,
                                                                 const float* __restrict__ c, int k,
-                                                                float* __restrict__ out, uint16_t* __restrict__ out16) {
+                                                                float* __restrict__ out, uint16_t* __restrict__ out16,
+                                                                const int32_t* __restrict__ seg_off = nullptr,
+                                                                const int32_t* __restrict__ seg_tile_off = nullptr,
+                                                                int n_seg = 0) {
   __shared__ float xs[kPdTile][33];
   __shared__ float cs[kPdTile][33];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int64_t r0 = (int64_t)blockIdx.x * kPdTile;
+  int64_t r0 = (int64_t)blockIdx.x * kPdTile;
   const int c0 = blockIdx.y * kPdTile;
+  int64_t seg_base = 0;
+  if (SEG) {
+    const int s = seg_of(seg_tile_off, n_seg, blockIdx.x);
+    seg_base = seg_off[s];
+    r0 = seg_base + (int64_t)(blockIdx.x - seg_tile_off[s]) * kPdTile;
+    n = seg_off[s + 1];               // rows end at the segment's end
+    c += (int64_t)s * k * dim;         // the segment's own centres
+    out16 += (int64_t)k * seg_base;    // its [k][n_s] block
+  }
+  const int64_t n_s = n - seg_base;   // row stride of the worker-major output
   float acc[4][4] = {};
   float xq[4] = {}, cq[4] = {};
   for (int d0 = 0; d0 < dim; d0 += 32) {
@@ -374,10 +401,10 @@ __global__ __launch_bounds__(256) void pairwise_distance_kernel(const float* __r
       if (MODE == 0) {
         out[rr * k + cc] = d;
       } else if (MODE == 1) {
-        out16[(int64_t)cc * n + rr] = __builtin_bit_cast(uint16_t, (_Float16)(-d));
+        out16[(int64_t)cc * n_s + (rr - seg_base)] = __builtin_bit_cast(uint16_t, (_Float16)(-d));
       } else {
         const _Float16 dh = (_Float16)d, lo = (_Float16)1e-5f;
-        out16[(int64_t)cc * n + rr] = __builtin_bit_cast(uint16_t, (_Float16)(-(dh < lo ? lo : dh)));
+        out16[(int64_t)cc * n_s + (rr - seg_base)] = __builtin_bit_cast(uint16_t, (_Float16)(-(dh < lo ? lo : dh)));
       }
     }
   }
@@ -625,6 +652,23 @@ int rqsid_auction_scores(const float* x, int64_t n, int32_t dim, const float* ce
     hipLaunchKernelGGL(pairwise_distance_kernel<1>, g, dim3(256), 0, (hipStream_t)stream, x, n, dim, centers, k,
                        (float*)nullptr, out_wj);
   return check_launch("auction_scores");
+}
+
+int rqsid_seg_auction_scores(const float* x, int64_t n, int32_t dim, const float* centers, int32_t k,
+                             int32_t n_seg, const int32_t* seg_off, const int32_t* seg_tile_off, int64_t n_tiles,
+                             int32_t half, uint16_t* out_wj, void* stream) {
+  if (!x || !centers || !out_wj || !seg_off || !seg_tile_off || n < 0 || k <= 0 || dim <= 0 || dim % 32 ||
+      n_seg <= 0 || n_tiles < 0 || n_tiles > INT32_MAX)
+    return fail(RQSID_E_ARG, "seg_auction_scores: bad arguments");
+  if (n == 0 || n_tiles == 0) return RQSID_OK;
+  const dim3 g((unsigned)n_tiles, (unsigned)cdiv(k, kPdTile));
+  if (half)
+    hipLaunchKernelGGL((pairwise_distance_kernel<2, true>), g, dim3(256), 0, (hipStream_t)stream, x, n, dim, centers,
+                       k, (float*)nullptr, out_wj, seg_off, seg_tile_off, n_seg);
+  else
+    hipLaunchKernelGGL((pairwise_distance_kernel<1, true>), g, dim3(256), 0, (hipStream_t)stream, x, n, dim, centers,
+                       k, (float*)nullptr, out_wj, seg_off, seg_tile_off, n_seg);
+  return check_launch("seg_auction_scores");
 }
 
 int rqsid_greedy_match(const float* dist, const int32_t* sub_off, int32_t groups, int32_t n_cand, int32_t max_take,

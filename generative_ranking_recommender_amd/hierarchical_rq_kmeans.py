@@ -33,7 +33,7 @@ import numpy as np
 import torch
 
 from . import ops
-from .balancekmeans import KMeans, _device
+from .balancekmeans import KMeans, _device, batched_fit, init_indices
 
 logger = logging.getLogger(__name__)
 
@@ -230,6 +230,11 @@ class HierarchicalRQKMeans:
         self.cluster_centers_list: List[torch.Tensor] = []
         self.match_matrices: List[np.ndarray] = []
         self.result_cluster_ids: List[torch.Tensor] = []
+        # Sub-K-Means of the middle layer and of the last-layer match matrix: True runs them in lockstep
+        # (balancekmeans.batched_fit: one segmented auction per iteration for all parents / groups);
+        # False runs them one after another as the reference does.  Both draw the numpy RNG in the
+        # reference's segment order; see batched_fit for the one schedule difference (early convergence).
+        self.batched_sub_fits = True
 
     @staticmethod
     def _get_device() -> torch.device:
@@ -339,6 +344,10 @@ class HierarchicalRQKMeans:
             if idx > layer:
                 target *= v
         order, off = group_rows(prev, pre_need)
+        if self.batched_sub_fits:
+            centers = self._batched_middle_fits(X, order, off, cur_need, layer, target)
+            raw, residual = self._reassign_clusters_middle_layer_with_residuals(X, centers, prev, layer)
+            return centers, raw % cur_need, residual
         sub_centers = []
         for i in range(pre_need):
             idx = order[off[i]:off[i + 1]]
@@ -351,6 +360,23 @@ class HierarchicalRQKMeans:
         centers = torch.cat(sub_centers, 0).contiguous()
         raw, residual = self._reassign_clusters_middle_layer_with_residuals(X, centers, prev, layer)
         return centers, raw % cur_need, residual
+
+    def _batched_middle_fits(self, X, order, off, cur_need, layer, target):
+        """The per-parent balanced fit_by_min_loss runs of :703-725 in lockstep.  Draws, in parent order,
+        each parent's start and every re-initialisation its iteration budget allows (the reference draws a
+        re-initialisation only while the fit has not converged)."""
+        cfg = self.config
+        sizes = np.diff(off).astype(np.int64)
+        limits, inits = [], []
+        for i, n_i in enumerate(sizes):
+            it = adaptive_iter_limit(int(n_i), cur_need, layer, cfg.iter_limit, is_sub_cluster=True)
+            limits.append(it)
+            inits.append([init_indices(int(n_i), cur_need) for _ in range(1 + max(0, (it - 1) // 10))])
+        layout = ops.SegmentLayout(sizes, self.device)
+        xs = X[order].contiguous()
+        centers, _ = batched_fit(xs, layout, cur_need, limits, inits, target_nodes_num=target,
+                                 half=cur_need >= 512)
+        return centers.contiguous()
 
     def _reassign_clusters_middle_layer_with_residuals(self, X, kmeans_centers, prev_cluster_ids, layer):
         """:839-904: each row may take only its parent's block of need[l] centres."""
@@ -435,6 +461,8 @@ class HierarchicalRQKMeans:
             rows, _ = ops.greedy_match(dist, sub_off, need)
             return rows.cpu().numpy()
 
+        if self.batched_sub_fits:
+            return self._batched_match_matrix(cand, X, order, off, G, need, cur_trunct_cluster, layer, greedy, match)
         for g in range(G):
             n_g = int(off[g + 1] - off[g])
             if n_g == 0:
@@ -458,6 +486,48 @@ class HierarchicalRQKMeans:
                 deferred_centers.append(centers)
         if deferred_groups:
             match[np.asarray(deferred_groups)] = greedy(deferred_groups, deferred_centers)
+        return match
+
+    def _batched_match_matrix(self, cand, X, order, off, G, need, trunc, layer, greedy, match):
+        """:968-1053 with the groups' sub-K-Means in lockstep (balancekmeans.batched_fit).  Every random
+        draw of the reference happens in its group order: a short group's random fill right after its
+        greedy step (its centres are its own rows, so the greedy step can run first), a mid-size group's
+        row sample, a large group's initialisation (``fit`` draws nothing else from numpy)."""
+        sizes = np.diff(off).astype(np.int64)
+        short = [g for g in range(G) if 0 < sizes[g] < need]
+        if short:
+            rows = greedy(short, [X[order[off[g]:off[g + 1]]] for g in short])
+            for g, r in zip(short, rows):
+                match[g] = r
+        full_groups, full_centers = [], {}
+        big, big_inits = [], []
+        for g in range(G):
+            n_g = int(sizes[g])
+            if n_g == 0:
+                continue
+            if n_g < need:
+                random_fill(match[g], need)
+            elif n_g == need:
+                full_groups.append(g)
+                full_centers[g] = X[order[off[g]:off[g + 1]]]
+            elif n_g < trunc:
+                sub = X[order[off[g]:off[g + 1]]]
+                full_groups.append(g)
+                full_centers[g] = sub[torch.from_numpy(np.random.choice(n_g, need, replace=False)).to(self.device)]
+            else:
+                full_groups.append(g)
+                big.append(g)
+                big_inits.append([init_indices(n_g, need)])
+        if big:
+            bsz = sizes[big]
+            layout = ops.SegmentLayout(bsz, self.device)
+            rows = torch.cat([order[off[g]:off[g + 1]] for g in big])
+            limits = [adaptive_iter_limit(int(n), need, layer, base_iter_limit=20) for n in bsz]
+            centers, _ = batched_fit(X[rows].contiguous(), layout, need, limits, big_inits, half=False)
+            for i, g in enumerate(big):
+                full_centers[g] = centers[i * need:(i + 1) * need]
+        if full_groups:
+            match[np.asarray(full_groups)] = greedy(full_groups, [full_centers[g] for g in full_groups])
         return match
 
     def _load_previous_checkpoints(self, start_layer: int):

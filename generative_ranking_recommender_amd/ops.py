@@ -357,3 +357,71 @@ def centroid_sums(x: torch.Tensor, assignment: torch.Tensor, k: int):
                                                _ptr(b.seg_tile_off), b.max_tiles, _ptr(sums), _stream()),
                "rqsid_centroid_accumulate")
     return sums, b.seg_row_off[1:] - b.seg_row_off[:-1]
+
+
+class SegmentLayout:
+    """Rows grouped by segment (segment s = rows off[s] .. off[s+1] of a segment-ordered matrix), with the
+    tile and chunk tables of the segmented auction kernels (include/rqsid.h rqsid_seg_auction_*)."""
+
+    def __init__(self, sizes, device):
+        import numpy as np
+        sizes = np.asarray(sizes, dtype=np.int64)
+        if sizes.ndim != 1 or len(sizes) == 0 or (sizes < 0).any():
+            raise ValueError("segment sizes must be a non-empty 1-D array of counts")
+        self.sizes = sizes
+        self.n_seg = len(sizes)
+        off = np.zeros(self.n_seg + 1, dtype=np.int64)
+        off[1:] = np.cumsum(sizes)
+        if off[-1] > 2**31 - 1:
+            raise ValueError("segmented auction: more than 2^31 - 1 rows")
+        self.off = off
+        self.n = int(off[-1])
+        tiles = (sizes + 63) // 64
+        ch = int(lib().rqsid_seg_auction_chunk_jobs())
+        chunks = (sizes + ch - 1) // ch
+        toff = np.concatenate([[0], np.cumsum(tiles)])
+        coff = np.concatenate([[0], np.cumsum(chunks)])
+        self.n_tiles = int(toff[-1])
+        self.total_chunks = int(coff[-1])
+        self.n_multi = int((chunks > 1).sum())
+        self.seg_off = torch.as_tensor(off, dtype=torch.int32).to(device)
+        self.tile_off = torch.as_tensor(toff, dtype=torch.int32).to(device)
+        self.chunk_off = torch.as_tensor(coff, dtype=torch.int32).to(device)
+        self.seg_of_row = torch.repeat_interleave(torch.arange(self.n_seg, device=device),
+                                                  torch.as_tensor(sizes).to(device))
+
+
+def seg_auction_scores(x: torch.Tensor, centers: torch.Tensor, k: int, layout: SegmentLayout,
+                       half: bool = False) -> torch.Tensor:
+    """Per-segment worker-major fp16 scores -distance (segment s: rows of layout, centres s*k..s*k+k-1),
+    concatenated: a flat fp16 tensor of k * N values."""
+    centers = centers.float().contiguous()
+    _require_device(x, centers)
+    n, d = x.shape
+    if n != layout.n or centers.shape[0] != layout.n_seg * k or centers.shape[1] != d:
+        raise ValueError("seg_auction_scores: rows / centres do not match the segment layout")
+    out = torch.empty(max(k * n, 1), dtype=torch.float16, device=x.device)
+    _lib.check(lib().rqsid_seg_auction_scores(_ptr(x), n, d, _ptr(centers), k, layout.n_seg, _ptr(layout.seg_off),
+                                              _ptr(layout.tile_off), layout.n_tiles, int(half), _ptr(out), _stream()),
+               "rqsid_seg_auction_scores")
+    return out
+
+
+def seg_auction(scores: torch.Tensor, k: int, layout: SegmentLayout, active: Optional[torch.Tensor] = None,
+                max_rounds: int = 0, out: Optional[torch.Tensor] = None):
+    """One balanced auction per segment, all advanced in lockstep.  Returns (assignment i32 [N] local to
+    each segment, rounds i32 [S] on the device).  Segments with active[s] == 0 keep ``out``'s entries."""
+    scores = scores.to(torch.float16).contiguous()
+    _require_device(scores, active)
+    n = layout.n
+    if out is None:
+        out = torch.full((max(n, 1),), -1, dtype=torch.int32, device=scores.device)
+    rounds = torch.zeros(layout.n_seg, dtype=torch.int32, device=scores.device)
+    wsb = int(lib().rqsid_seg_auction_workspace_bytes(n, k, layout.n_seg, layout.total_chunks, layout.n_multi))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=scores.device)
+    act = None if active is None else active.to(torch.uint8).contiguous()
+    _lib.check(lib().rqsid_seg_auction_lap_half(_ptr(scores), k, layout.n_seg, _ptr(layout.seg_off),
+                                                _ptr(layout.chunk_off), layout.total_chunks, layout.n_multi, n,
+                                                _ptr(act), int(max_rounds), _ptr(out), _ptr(rounds), _ptr(ws), wsb,
+                                                _stream()), "rqsid_seg_auction_lap_half")
+    return out[:n], rounds

@@ -177,6 +177,36 @@ int rqsid_auction_lap_half(const uint16_t* scores_wj, int32_t n_workers, int64_t
                            int32_t max_rounds, int32_t* out_assign, int32_t* out_rounds,
                            void* workspace, int64_t workspace_bytes, void* stream);
 
+/* Segmented auction scores for many independent balanced fits at once (the per-parent sub-K-Means of
+ * hierarchical_rq_kmeans.py:671-752 and the per-group sub-K-Means of :968-1053, which the reference runs
+ * one after another, each through balancekmeans/__init__.py:29-43,536-603).  Segment s owns rows
+ * seg_off[s] .. seg_off[s+1] of x (rows grouped by segment) and centres s*k .. s*k+k-1; its scores go to
+ * out_wj + k*seg_off[s] as a [k][n_s] worker-major block, each value equal to rqsid_auction_scores on the
+ * segment alone.  seg_tile_off[S+1] = exclusive scan of ceil(n_s / 64); n_tiles = seg_tile_off[S]. */
+int rqsid_seg_auction_scores(const float* x, int64_t n, int32_t dim, const float* centers, int32_t k,
+                             int32_t n_seg, const int32_t* seg_off, const int32_t* seg_tile_off,
+                             int64_t n_tiles, int32_t half, uint16_t* out_wj, void* stream);
+
+/* Segmented balanced assignment: one auction_lap_half (balancekmeans/__init__.py:12-140) per segment, all
+ * segments advanced in lockstep (one launch sequence per round for all of them; a segment stops at its own
+ * round count).  Segment s: jobs seg_off[s] .. seg_off[s+1] (n_s), scores at scores + k*seg_off[s] as
+ * [k][n_s] fp16 (the layout of rqsid_seg_auction_scores).  Jobs are cut into chunks of
+ * rqsid_seg_auction_chunk_jobs() that never straddle segments: seg_chunk_off[S+1] = exclusive scan of
+ * ceil(n_s / chunk), total_chunks = seg_chunk_off[S]; n_multi = number of segments of more than one chunk
+ * (checked).  active[s] (NULL = all) == 0 skips a segment (its out_assign entries are untouched).
+ * out_assign[j] = worker of job j inside its segment; out_rounds[s] (device) = rounds run (0 for the
+ * n_s < k fallback, argmin(-D) = the farthest centre, as the reference).  Each segment's result is
+ * bit-identical to rqsid_auction_lap_half on its block alone.  Blocks the calling thread (one host read per
+ * 8 rounds).  max_rounds <= 0: unbounded. */
+int32_t rqsid_seg_auction_chunk_jobs(void);
+int64_t rqsid_seg_auction_workspace_bytes(int64_t n_jobs, int32_t n_workers, int32_t n_seg,
+                                          int64_t total_chunks, int32_t n_multi);
+int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_t n_seg,
+                               const int32_t* seg_off, const int32_t* seg_chunk_off, int64_t total_chunks,
+                               int32_t n_multi, int64_t n_jobs, const uint8_t* active, int32_t max_rounds,
+                               int32_t* out_assign, int32_t* out_rounds, void* workspace,
+                               int64_t workspace_bytes, void* stream);
+
 /* Greedy unique-nearest match rows (_assign_last_match_matrix hierarchical_rq_kmeans.py:1022-1038,
  * _get_dynamic_match_matrix simplified_semantic_id_generator.py:282-291): group g owns rows
  * sub_off[g]..sub_off[g+1] of dist [total][n_cand]; its first min(rows, max_take) rows each take, in
