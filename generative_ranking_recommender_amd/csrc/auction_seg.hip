@@ -15,6 +15,7 @@
 // ceil(N_s / kCh)).  A segment of one chunk (the last layer's groups: median ~600 rows) selects its
 // per-worker thresholds inside one block from LDS histograms (sa_small_select_kernel); wider segments
 // (the middle layer's parents) use per-(segment, worker) global histograms like auction.hip.
+#include <algorithm>
 #include <cmath>
 
 #include "internal.h"
@@ -52,6 +53,7 @@ struct SegAuction {
   uint32_t* mm;                  // [S][2] max key, min key
   uint32_t* have;                // [S] jobs with a bidder this round
   int32_t* rounds;               // [S] rounds run (device)
+  int32_t* round_dev;            // [1] the current round (device, so a captured block of rounds replays)
   uint32_t* live_count;          // [1]
   uint16_t* cost;                // [N]
   int32_t* hb;                   // [N]
@@ -118,6 +120,7 @@ __global__ __launch_bounds__(256) void sa_seg_init_kernel(SegAuction a, const ui
   a.mm[2 * s + 1] = 0xFFFFFFFFu;
   a.have[s] = 0;
   a.rounds[s] = 0;
+  if (s == 0) *a.round_dev = 0;
 }
 
 __global__ __launch_bounds__(256) void sa_job_init_kernel(SegAuction a, int64_t n) {
@@ -383,7 +386,8 @@ __global__ __launch_bounds__(256) void sa_eqscan_kernel(SegAuction a) {
 }
 
 // ---- bids: one packed {fp16 bid, ~worker} atomicMax per job and block ----
-__global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a, int counter) {
+__global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a) {
+  const int counter = *a.round_dev;
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
   if (!(f & kLive)) return;
@@ -465,7 +469,10 @@ __global__ __launch_bounds__(256) void sa_resolve_kernel(SegAuction a, int32_t* 
 }
 
 // end of round r: a segment whose every job has a bidder is done after r+1 rounds
-__global__ __launch_bounds__(256) void sa_round_end_kernel(SegAuction a, int round, int count) {
+__global__ void sa_round_inc_kernel(SegAuction a) { *a.round_dev += 1; }
+
+__global__ __launch_bounds__(256) void sa_round_end_kernel(SegAuction a, int count) {
+  const int round = *a.round_dev;
   const int s = blockIdx.x * 256 + threadIdx.x;
   uint32_t live = 0;
   if (s < a.S && (a.flag[s] & kLive)) {
@@ -529,6 +536,7 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.mm = c.take<uint32_t>(2 * (int64_t)S);
   a.have = c.take<uint32_t>(S);
   a.live_count = c.take<uint32_t>(2);
+  a.round_dev = c.take<int32_t>(1);
   a.hidx = c.take<int32_t>(S);
   a.mseg = c.take<int32_t>(a.n_multi > 0 ? a.n_multi : 1);
   a.cost = c.take<uint16_t>(N);
@@ -621,35 +629,66 @@ int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_
     (void)hipHostFree(host);
     return rc;
   }
-  // The live count is read back every kPoll rounds (rounds of finished segments are no-ops, so polling
-  // late only costs a few empty launches); only the polled round counts, into a zeroed counter.
+  // Rounds run in blocks of kPoll: the live count is read back after each block (rounds of finished
+  // segments are no-ops, so stopping late only costs empty launches) and only a block's last round counts,
+  // into a counter zeroed after each read.  The round number lives on the device, so one captured block
+  // (a HIP graph of kPoll rounds) replays for every block: the auction is launch-bound at small N.
   constexpr int kPoll = 8;
-  if (hipMemsetAsync(a.live_count, 0, 4, st) != hipSuccess) rc = fail(RQSID_E_LAUNCH, "seg_auction: memset");
-  for (int round = 0; rc == RQSID_OK && (max_rounds <= 0 || round < max_rounds); ++round) {
+  auto launch_round = [&](hipStream_t q, bool count) {
     if (n_multi > 0) {
-      hipLaunchKernelGGL((sa_hist_kernel<false>), gcw, dim3(256), 0, st, a);
-      hipLaunchKernelGGL((sa_select_kernel<false>), dim3(gmw), dim3(256), 0, st, a);
-      hipLaunchKernelGGL((sa_hist_kernel<true>), gcw, dim3(256), 0, st, a);
-      hipLaunchKernelGGL((sa_select_kernel<true>), dim3(gmw), dim3(256), 0, st, a);
-      hipLaunchKernelGGL(sa_eqcount_kernel, gcw, dim3(256), 0, st, a);
-      hipLaunchKernelGGL(sa_eqscan_kernel, dim3(gmw), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((sa_hist_kernel<false>), gcw, dim3(256), 0, q, a);
+      hipLaunchKernelGGL((sa_select_kernel<false>), dim3(gmw), dim3(256), 0, q, a);
+      hipLaunchKernelGGL((sa_hist_kernel<true>), gcw, dim3(256), 0, q, a);
+      hipLaunchKernelGGL((sa_select_kernel<true>), dim3(gmw), dim3(256), 0, q, a);
+      hipLaunchKernelGGL(sa_eqcount_kernel, gcw, dim3(256), 0, q, a);
+      hipLaunchKernelGGL(sa_eqscan_kernel, dim3(gmw), dim3(256), 0, q, a);
     }
-    if (any_single) hipLaunchKernelGGL(sa_small_select_kernel, gcw, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(sa_bid_kernel, gcw, dim3(256), 0, st, a, round);
-    hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, st, a, out_assign);
-    const bool last = max_rounds > 0 && round + 1 >= max_rounds;
-    const bool poll = (round + 1) % kPoll == 0 || last;
-    hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, st, a, round, (int)poll);
+    if (any_single) hipLaunchKernelGGL(sa_small_select_kernel, gcw, dim3(256), 0, q, a);
+    hipLaunchKernelGGL(sa_bid_kernel, gcw, dim3(256), 0, q, a);
+    hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, q, a, out_assign);
+    hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
+    hipLaunchKernelGGL(sa_round_inc_kernel, dim3(1), dim3(1), 0, q, a);
+  };
+  // capture one block on a private stream (the caller's may be the null stream, which cannot capture)
+  hipGraphExec_t exec = nullptr;
+  {
+    hipStream_t cs = nullptr;
+    hipGraph_t graph = nullptr;
+    if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) == hipSuccess) {
+      if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) == hipSuccess) {
+        for (int i = 0; i < kPoll; ++i) launch_round(cs, i == kPoll - 1);
+        if (hipStreamEndCapture(cs, &graph) == hipSuccess && graph) {
+          if (hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) != hipSuccess) exec = nullptr;
+          (void)hipGraphDestroy(graph);
+        }
+      }
+      (void)hipStreamDestroy(cs);
+    }
+    (void)hipGetLastError();  // a failed capture falls back to direct launches
+  }
+  if (hipMemsetAsync(a.live_count, 0, 4, st) != hipSuccess) rc = fail(RQSID_E_LAUNCH, "seg_auction: memset");
+  for (int done = 0; rc == RQSID_OK && (max_rounds <= 0 || done < max_rounds);) {
+    const int n = max_rounds > 0 ? std::min(kPoll, max_rounds - done) : kPoll;
+    if (exec && n == kPoll) {
+      if (hipGraphLaunch(exec, st) != hipSuccess) {
+        rc = fail(RQSID_E_LAUNCH, "seg_auction: graph launch");
+        break;
+      }
+    } else {
+      for (int i = 0; i < n; ++i) launch_round(st, i == n - 1);
+    }
+    done += n;
     if ((rc = check_launch("seg_auction_round"))) break;
-    if (!poll) continue;
     if (hipMemcpyAsync(host, a.live_count, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemsetAsync(a.live_count, 0, 4, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
       rc = fail(RQSID_E_LAUNCH, "seg_auction: readback");
       break;
     }
     if (host[0] == 0) break;
-    if (last) rc = fail(RQSID_E_LAUNCH, "seg_auction: %u segments still bidding after %d rounds", host[0], max_rounds);
+    if (max_rounds > 0 && done >= max_rounds)
+      rc = fail(RQSID_E_LAUNCH, "seg_auction: %u segments still bidding after %d rounds", host[0], max_rounds);
   }
+  if (exec) (void)hipGraphExecDestroy(exec);
   (void)hipHostFree(host);
   return rc;
 }

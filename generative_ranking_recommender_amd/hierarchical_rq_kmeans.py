@@ -203,14 +203,31 @@ def group_rows(keys: torch.Tensor, n_groups: int):
 
 
 def random_fill(row: np.ndarray, need: int) -> None:
-    """The reference's fill-up loop (hierarchical :1041-1048 / simplified :294-297)."""
+    """The reference's fill-up loop (hierarchical :1041-1048 / simplified :294-297):
+    ``while have < need: r = np.random.randint(n_cand); if not row[r]: row[r] = 1; have += 1``.
+
+    Drawn in blocks: the legacy MT19937 ``randint(n, size=m)`` yields exactly the values (and the
+    generator state) of m single calls, so a block is drawn, scanned in draw order for the first
+    occurrences of unset columns, and when the block holds the last needed column the generator is
+    rewound and advanced by exactly the draws the loop would have consumed."""
     n_cand = row.shape[0]
     have = int(row.sum())
     while have < need:
-        r = np.random.randint(n_cand)
-        if not row[r]:
-            row[r] = 1
-            have += 1
+        state = np.random.get_state()
+        m = max(64, 2 * (need - have))
+        draws = np.random.randint(n_cand, size=m)
+        vals, first = np.unique(draws, return_index=True)
+        fresh = row[vals] == 0
+        pos = np.sort(first[fresh])
+        missing = need - have
+        if len(pos) >= missing:
+            k = int(pos[missing - 1])
+            np.random.set_state(state)
+            np.random.randint(n_cand, size=k + 1)
+            row[draws[pos[:missing]]] = 1
+            return
+        row[draws[pos]] = 1
+        have += len(pos)
 
 
 def masked_assign(x: torch.Tensor, centers: torch.Tensor, seg: torch.Tensor, cand: ops.Candidates, n_segments: int):
@@ -345,7 +362,9 @@ class HierarchicalRQKMeans:
                 target *= v
         order, off = group_rows(prev, pre_need)
         if self.batched_sub_fits:
+            t0 = time.time()
             centers = self._batched_middle_fits(X, order, off, cur_need, layer, target)
+            logger.info("[LAYER %d] %d lockstep sub-fits %.2fs", layer + 1, pre_need, time.time() - t0)
             raw, residual = self._reassign_clusters_middle_layer_with_residuals(X, centers, prev, layer)
             return centers, raw % cur_need, residual
         sub_centers = []
@@ -395,18 +414,22 @@ class HierarchicalRQKMeans:
             raise RuntimeError(
                 f"Previous layers cluster IDs not found. "
                 f"Expected at least 2 layers but only have {len(self.result_cluster_ids)} layers.")
+        t0 = time.time()
         parts = []
         for _ in range(2):
             km = KMeans(n_clusters=n_clusters, device=self.device, balanced=True)
             km.fit(X=X, distance="euclidean", iter_limit=20, tqdm_flag=True, half=n_clusters >= 512, online=False)
             parts.append(km.cluster_centers.detach())
         cand_centers = torch.cat(parts, 0).contiguous()
+        logger.info("[LAYER %d] candidate fits (2 x %d centres) %.2fs", layer + 1, n_clusters, time.time() - t0)
+        t0 = time.time()
         l1 = self.result_cluster_ids[-2].to(self.device).long()
         l2 = self.result_cluster_ids[-1].to(self.device).long()
         pp_need = cfg.need_clusters[layer - 2]
         match = self._assign_last_match_matrix(cand_centers, 2 * n_clusters, X, pp_need, cfg.need_clusters[layer - 1],
                                                l1, l2, need, 2 * need, layer)
         self.match_matrices.append(match)
+        logger.info("[LAYER %d] match matrix %.2fs", layer + 1, time.time() - t0)
         before = l1 * pp_need + l2
         raw, residual = self._reassign_clusters_last_layer_with_residuals(X, cand_centers, before, match, layer)
         ids = self._merge_match_matrix_cluster_ids(match, raw, before)
@@ -492,15 +515,24 @@ class HierarchicalRQKMeans:
         """:968-1053 with the groups' sub-K-Means in lockstep (balancekmeans.batched_fit).  Every random
         draw of the reference happens in its group order: a short group's random fill right after its
         greedy step (its centres are its own rows, so the greedy step can run first), a mid-size group's
-        row sample, a large group's initialisation (``fit`` draws nothing else from numpy)."""
+        row sample, a large group's initialisation (``fit`` draws nothing else from numpy).  Rows are
+        gathered once for all groups (16384 groups at PROD shape)."""
         sizes = np.diff(off).astype(np.int64)
+
+        def rows_of(groups, picks=None):
+            """positions in ``order`` of each group's rows (or of its picked rows), concatenated"""
+            parts = [off[g] + (np.arange(sizes[g]) if picks is None else picks[i]) for i, g in enumerate(groups)]
+            return torch.from_numpy(np.concatenate(parts).astype(np.int64)).to(self.device)
+
+        def greedy_cat(sc, counts):
+            sub_off = torch.tensor(np.concatenate([[0], np.cumsum(counts)]), dtype=torch.int32, device=self.device)
+            rows, _ = ops.greedy_match(ops.pairwise_distance(sc.float().contiguous(), cand), sub_off, need)
+            return rows.cpu().numpy()
+
         short = [g for g in range(G) if 0 < sizes[g] < need]
         if short:
-            rows = greedy(short, [X[order[off[g]:off[g + 1]]] for g in short])
-            for g, r in zip(short, rows):
-                match[g] = r
-        full_groups, full_centers = [], {}
-        big, big_inits = [], []
+            match[np.asarray(short)] = greedy_cat(X[order[rows_of(short)]], sizes[short])
+        small, small_picks, big, big_inits = [], [], [], []
         for g in range(G):
             n_g = int(sizes[g])
             if n_g == 0:
@@ -508,26 +540,30 @@ class HierarchicalRQKMeans:
             if n_g < need:
                 random_fill(match[g], need)
             elif n_g == need:
-                full_groups.append(g)
-                full_centers[g] = X[order[off[g]:off[g + 1]]]
+                small.append(g)
+                small_picks.append(np.arange(n_g))
             elif n_g < trunc:
-                sub = X[order[off[g]:off[g + 1]]]
-                full_groups.append(g)
-                full_centers[g] = sub[torch.from_numpy(np.random.choice(n_g, need, replace=False)).to(self.device)]
+                small.append(g)
+                small_picks.append(np.asarray(np.random.choice(n_g, need, replace=False)))
             else:
-                full_groups.append(g)
                 big.append(g)
                 big_inits.append([init_indices(n_g, need)])
+        centers = {}
+        if small:
+            sc = X[order[rows_of(small, small_picks)]]
+            for i, g in enumerate(small):
+                centers[g] = sc[i * need:(i + 1) * need]
         if big:
             bsz = sizes[big]
             layout = ops.SegmentLayout(bsz, self.device)
-            rows = torch.cat([order[off[g]:off[g + 1]] for g in big])
             limits = [adaptive_iter_limit(int(n), need, layer, base_iter_limit=20) for n in bsz]
-            centers, _ = batched_fit(X[rows].contiguous(), layout, need, limits, big_inits, half=False)
+            bc, _ = batched_fit(X[order[rows_of(big)]].contiguous(), layout, need, limits, big_inits, half=False)
             for i, g in enumerate(big):
-                full_centers[g] = centers[i * need:(i + 1) * need]
-        if full_groups:
-            match[np.asarray(full_groups)] = greedy(full_groups, [full_centers[g] for g in full_groups])
+                centers[g] = bc[i * need:(i + 1) * need]
+        full = sorted(centers)
+        if full:
+            match[np.asarray(full)] = greedy_cat(torch.cat([centers[g] for g in full], 0),
+                                                 np.full(len(full), need))
         return match
 
     def _load_previous_checkpoints(self, start_layer: int):

@@ -22,7 +22,7 @@ import torch
 
 from . import io as rq_io
 from . import ops
-from .balancekmeans import KMeans, _device
+from .balancekmeans import KMeans, _device, batched_fit, init_indices
 from .hierarchical_rq_kmeans import HierarchicalRQKMeansConfig, group_rows, masked_assign, random_fill
 
 logger = logging.getLogger(__name__)
@@ -36,6 +36,9 @@ class SimplifiedHierarchicalRQ:
         self.dynamic_match_matrix = None
         self.final_layer_centers = None
         self.middle_layer_centers = None
+        # per-parent / per-group sub-fits in lockstep (True) or one after another like the reference
+        # (False); both keep the reference's numpy draw order (``fit`` draws only its start)
+        self.batched_sub_fits = True
 
     def _load_data(self, data_path: str, limit: int = None):
         """:38-76 -> (song_ids, tensor fp16/fp32 on the host)."""
@@ -55,6 +58,47 @@ class SimplifiedHierarchicalRQ:
         prev_n_need = cfg.need_clusters[layer_idx - 1]
         use_half = n_clusters > 512
         order, off = group_rows(prev_cluster_ids, prev_n_need)
+        if self.batched_sub_fits:
+            combined = self._batched_middle_centers(data, order, off, prev_n_need, n_need, use_half)
+        else:
+            combined = self._sequential_middle_centers(data, order, off, prev_n_need, n_need, use_half)
+        self.middle_layer_centers = combined
+        cand = ops.contiguous_candidates(prev_n_need, n_need, self.device)
+        _, glob = masked_assign(data, combined, prev_cluster_ids, cand, prev_n_need)
+        residuals = ops.residual(data, combined, glob, normalize=False)
+        return glob.long() % n_need, residuals
+
+    def _batched_middle_centers(self, data, order, off, prev_n_need, n_need, use_half):
+        """The per-parent ``fit`` runs of :98-140 in lockstep (balancekmeans.batched_fit).  ``fit`` draws
+        only its start from numpy, so drawing every parent's start (or its with-replacement sample when
+        it has fewer rows than centres) in parent order keeps the reference's RNG sequence."""
+        sizes = np.diff(off).astype(np.int64)
+        d = data.shape[1]
+        picks, fits, inits = {}, [], []
+        for i in range(prev_n_need):
+            n_i = int(sizes[i])
+            if n_i == 0:
+                continue
+            if n_i < n_need:
+                picks[i] = np.asarray(np.random.choice(n_i, n_need, replace=True))
+            else:
+                fits.append(i)
+                inits.append([init_indices(n_i, n_need)])
+        out = torch.zeros(prev_n_need * n_need, d, device=self.device)
+        for i, p in picks.items():
+            out[i * n_need:(i + 1) * n_need] = data[order[off[i] + torch.from_numpy(p).to(self.device)]]
+        if fits:
+            fsz = sizes[fits]
+            rows = torch.from_numpy(np.concatenate([np.arange(off[i], off[i + 1]) for i in fits])).to(self.device)
+            c, _ = batched_fit(data[order[rows]].contiguous(), ops.SegmentLayout(fsz, self.device), n_need,
+                               [self.config.iter_limit] * len(fits), inits, half=use_half)
+            sel = torch.cat([torch.arange(i * n_need, (i + 1) * n_need) for i in fits]).to(self.device)
+            out[sel] = c
+        return out.contiguous()
+
+    def _sequential_middle_centers(self, data, order, off, prev_n_need, n_need, use_half):
+        """:98-140 one parent after another (the reference's order)."""
+        cfg = self.config
         subs = []
         for i in range(prev_n_need):
             n_i = int(off[i + 1] - off[i])
@@ -68,12 +112,7 @@ class SimplifiedHierarchicalRQ:
                 km = KMeans(n_clusters=n_need, device=self.device, balanced=True)
                 km.fit(X=sub, iter_limit=cfg.iter_limit, half=use_half, tqdm_flag=False)
                 subs.append(km.cluster_centers)
-        combined = torch.cat(subs).float().contiguous()
-        self.middle_layer_centers = combined
-        cand = ops.contiguous_candidates(prev_n_need, n_need, self.device)
-        _, glob = masked_assign(data, combined, prev_cluster_ids, cand, prev_n_need)
-        residuals = ops.residual(data, combined, glob, normalize=False)
-        return glob.long() % n_need, residuals
+        return torch.cat(subs).float().contiguous()
 
     def train(self, data_path: str, data_limit: int = None):
         """:176-245."""
@@ -136,6 +175,8 @@ class SimplifiedHierarchicalRQ:
             rows, _ = ops.greedy_match(ops.pairwise_distance(sc, candidate_centers), sub_off, max(sizes))
             return rows.cpu().numpy()
 
+        if self.batched_sub_fits:
+            return self._batched_dynamic_match(data, order, off, G, n_need, candidate_centers, match)
         for g in range(G):
             n_g = int(off[g + 1] - off[g])
             if n_g == 0:
@@ -155,6 +196,48 @@ class SimplifiedHierarchicalRQ:
                 deferred_c.append(centers)
         if deferred:
             match[np.asarray(deferred)] = greedy(deferred_c)
+        return torch.from_numpy(match.astype(np.float32))
+
+    def _batched_dynamic_match(self, data, order, off, G, n_need, candidate_centers, match):
+        """:247-303 with the groups' ``fit`` runs in lockstep; every numpy draw stays in group order (an
+        empty group's candidate sample, a short group's random fill after its greedy step, a large
+        group's start)."""
+        sizes = np.diff(off).astype(np.int64)
+        n_cand = candidate_centers.shape[0]
+
+        def greedy_cat(sc, counts):
+            sub_off = torch.tensor(np.concatenate([[0], np.cumsum(counts)]), dtype=torch.int32, device=self.device)
+            rows, _ = ops.greedy_match(ops.pairwise_distance(sc.float().contiguous(), candidate_centers), sub_off,
+                                       int(max(counts)))
+            return rows.cpu().numpy()
+
+        def rows_of(groups):
+            return torch.from_numpy(np.concatenate([np.arange(off[g], off[g + 1]) for g in groups])).to(self.device)
+
+        short = [g for g in range(G) if 0 < sizes[g] < n_need]
+        if short:
+            match[np.asarray(short)] = greedy_cat(data[order[rows_of(short)]], sizes[short])
+        centers, fits, inits = {}, [], []
+        for g in range(G):
+            n_g = int(sizes[g])
+            if n_g == 0:
+                centers[g] = candidate_centers[torch.from_numpy(np.random.choice(n_cand, n_need, replace=False))
+                                               .to(self.device)]
+            elif n_g < n_need:
+                random_fill(match[g], n_need)
+            elif n_g == n_need:
+                centers[g] = data[order[off[g]:off[g + 1]]]
+            else:
+                fits.append(g)
+                inits.append([init_indices(n_g, n_need)])
+        if fits:
+            c, _ = batched_fit(data[order[rows_of(fits)]].contiguous(), ops.SegmentLayout(sizes[fits], self.device),
+                               n_need, [20] * len(fits), inits)
+            for i, g in enumerate(fits):
+                centers[g] = c[i * n_need:(i + 1) * n_need]
+        full = sorted(centers)
+        if full:
+            match[np.asarray(full)] = greedy_cat(torch.cat([centers[g] for g in full], 0), np.full(len(full), n_need))
         return torch.from_numpy(match.astype(np.float32))
 
     def _predict_with_dynamic_matrix(self, data, prev_ids_l1, prev_ids_l2, candidate_centers, match_matrix):

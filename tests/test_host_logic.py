@@ -91,3 +91,32 @@ def test_statistics_side_file():
     l0 = st["layer_statistics"][0]
     assert l0["unique_clusters"] == 2 and l0["cluster_distribution"]["max"] == 2
     json.dumps(st)
+
+
+def test_random_fill_blocks_equal_the_reference_loop():
+    """hierarchical :1041-1048 / simplified :294-297 one draw at a time vs the block-drawn restatement:
+    same row, same numpy generator state afterwards."""
+    import numpy as np
+    from generative_ranking_recommender_amd.hierarchical_rq_kmeans import random_fill
+
+    def loop(row, need):
+        have = int(row.sum())
+        while have < need:
+            r = np.random.randint(row.shape[0])
+            if not row[r]:
+                row[r] = 1
+                have += 1
+
+    rng = np.random.default_rng(0)
+    for n_cand, need, pre in [(2560, 256, 3), (32, 8, 0), (300, 299, 10), (64, 64, 63), (5120, 512, 500), (16, 4, 4)]:
+        base = np.zeros(n_cand, np.uint8)
+        base[rng.choice(n_cand, pre, replace=False)] = 1
+        a, b = base.copy(), base.copy()
+        np.random.seed(n_cand + need)
+        loop(a, need)
+        sa = np.random.get_state()
+        np.random.seed(n_cand + need)
+        random_fill(b, need)
+        sb = np.random.get_state()
+        assert np.array_equal(a, b)
+        assert np.array_equal(sa[1], sb[1]) and sa[2] == sb[2]

@@ -1,0 +1,38 @@
+"""Time one balanced auction (rqsid_auction_lap_half) on random fp16 -distance scores.
+
+    python tools/auction_bench.py --jobs 100000 --workers 1280 [--reps 2]"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from generative_ranking_recommender_amd import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=100000)
+    ap.add_argument("--workers", type=int, default=1280)
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(a.jobs, 512, device="cuda", generator=g)
+    c = torch.randn(a.workers, 512, device="cuda", generator=g)
+    w = ops.auction_scores(x, c, half=True)
+    for r in range(a.reps):
+        torch.cuda.synchronize()
+        t = time.time()
+        _, rounds = ops.auction(w)
+        torch.cuda.synchronize()
+        dt = time.time() - t
+        print(json.dumps({"jobs": a.jobs, "workers": a.workers, "rounds": rounds, "s": round(dt, 3),
+                          "ms_per_round": round(1e3 * dt / max(rounds, 1), 4),
+                          "W_GB": round(2 * a.jobs * a.workers / 1e9, 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,69 @@
+"""Time HierarchicalRQKMeans.train at the PROD shape (layer_clusters [128,1280,1280], need [128,128,256])
+on synthetic rows, per layer, with the lockstep sub-fits (default) or the reference's sequential order.
+
+    python tools/train_bench.py --rows 200000 [--sequential] [--out gpurun_out/train.json]
+
+Prints one JSON line: rows, per-layer seconds, total seconds, sub-fit mode."""
+import argparse
+import json
+import logging
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from generative_ranking_recommender_amd import synth  # noqa: E402
+from generative_ranking_recommender_amd.hierarchical_rq_kmeans import (HierarchicalRQKMeans,  # noqa: E402
+                                                                       HierarchicalRQKMeansConfig)
+
+
+class LayerTimes(logging.Handler):
+    def __init__(self):
+        super().__init__()
+        self.t0 = time.time()
+        self.marks = []
+
+    def emit(self, record):
+        msg = record.getMessage()
+        if msg.startswith("[LAYER"):
+            self.marks.append((msg, time.time() - self.t0))
+            print(msg, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=200000)
+    ap.add_argument("--sequential", action="store_true")
+    ap.add_argument("--iter-limit", type=int, default=100)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    x = synth.small_mixture(a.rows, m=4096, seed=5)
+    cfg = HierarchicalRQKMeansConfig(layer_clusters=[128, 1280, 1280], need_clusters=[128, 128, 256],
+                                     embedding_dim=512, iter_limit=a.iter_limit)
+    h = LayerTimes()
+    lg = logging.getLogger("generative_ranking_recommender_amd.hierarchical_rq_kmeans")
+    lg.setLevel(logging.INFO)
+    lg.addHandler(h)
+    np.random.seed(42)
+    torch.manual_seed(42)
+    model = HierarchicalRQKMeans(cfg, device=torch.device("cuda", 0))
+    model.batched_sub_fits = not a.sequential
+    t = time.time()
+    res = model.train(x)
+    torch.cuda.synchronize()
+    total = time.time() - t
+    ids = np.stack([r.cpu().numpy() for r in res["cluster_ids"]], 1)
+    consistent = bool((model.predict(x, reference_quirks=False) == ids).all())
+    line = {"rows": a.rows, "mode": "sequential" if a.sequential else "lockstep", "total_s": round(total, 2),
+            "layers": [m for m in h.marks], "unique_ids": int(len(np.unique(ids, axis=0))),
+            "train_encode_consistent": consistent}
+    print(json.dumps(line), flush=True)
+    if a.out:
+        Path(a.out).write_text(json.dumps(line) + "\n")
+
+
+if __name__ == "__main__":
+    main()
