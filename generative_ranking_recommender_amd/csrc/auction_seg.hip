@@ -237,8 +237,13 @@ __global__ __launch_bounds__(256) void sa_hist_kernel(SegAuction a) {
     const int64_t j = ci.j0 + jj;
     const int32_t hbj = a.hb[j];
     const uint16_t cj = a.cost[j];
-    for (int g = 0; g < nw; ++g) {
-      const uint32_t k = okey(value_bits(w0 + g, wrow(a, ci, w0 + g)[j], hbj, cj));
+    uint16_t v[kKG];
+#pragma unroll
+    for (int g = 0; g < kKG; ++g) v[g] = g < nw ? wrow(a, ci, w0 + g)[j] : 0;  // all loads in flight first
+#pragma unroll
+    for (int g = 0; g < kKG; ++g) {
+      if (g >= nw) continue;
+      const uint32_t k = okey(value_bits(w0 + g, v[g], hbj, cj));
       if (!LOW) atomicAdd(&h[g][k >> 8], 1u);
       else if ((k >> 8) == b1[g]) atomicAdd(&h[g][k & 255], 1u);
     }
@@ -302,8 +307,13 @@ __global__ __launch_bounds__(256) void sa_small_select_kernel(SegAuction a) {
       const int64_t j = ci.j0 + jj;
       const int32_t hbj = a.hb[j];
       const uint16_t cj = a.cost[j];
-      for (int g = 0; g < nw; ++g) {
-        const uint32_t k = okey(value_bits(w0 + g, wrow(a, ci, w0 + g)[j], hbj, cj));
+      uint16_t v[kKG];
+#pragma unroll
+      for (int g = 0; g < kKG; ++g) v[g] = g < nw ? wrow(a, ci, w0 + g)[j] : 0;
+#pragma unroll
+      for (int g = 0; g < kKG; ++g) {
+        if (g >= nw) continue;
+        const uint32_t k = okey(value_bits(w0 + g, v[g], hbj, cj));
         if (pass == 0) atomicAdd(&h[g][k >> 8], 1u);
         else if ((k >> 8) == b1s[g]) atomicAdd(&h[g][k & 255], 1u);
       }
@@ -350,7 +360,12 @@ __global__ __launch_bounds__(256) void sa_eqcount_kernel(SegAuction a) {
     const int64_t j = ci.j0 + jj;
     const int32_t hbj = a.hb[j];
     const uint16_t cj = a.cost[j];
-    for (int g = 0; g < nw; ++g) cnt[g] += okey(value_bits(w0 + g, wrow(a, ci, w0 + g)[j], hbj, cj)) == T[g];
+    uint16_t v[kKG];
+#pragma unroll
+    for (int g = 0; g < kKG; ++g) v[g] = g < nw ? wrow(a, ci, w0 + g)[j] : 0;
+#pragma unroll
+    for (int g = 0; g < kKG; ++g)
+      if (g < nw) cnt[g] += okey(value_bits(w0 + g, v[g], hbj, cj)) == T[g];
   }
   for (int g = 0; g < nw; ++g) {
     uint32_t v = cnt[g];
@@ -391,54 +406,78 @@ __global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a) {
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
   if (!(f & kLive)) return;
-  __shared__ uint32_t wsum[kKG][4];
+  __shared__ uint32_t wcnt[kJPT][kKG][4];  // per (job slice, worker, wave): values equal to T
   const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
   const int64_t sw0 = (int64_t)ci.s * a.K + w0;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint16_t eps = a.eps[ci.s];
   const float epsf = h2f(eps);
   uint32_t T[kKG], need[kKG], off[kKG];
-  float vT[kKG];
   for (int g = 0; g < kKG; ++g) {
     T[g] = g < nw ? a.sel[(sw0 + g) * 4 + 2] : 0xFFFFFFFFu;
     need[g] = g < nw ? a.sel[(sw0 + g) * 4 + 3] : 0;
     off[g] = (g < nw && !(f & kSingle)) ? a.eqcnt[(int64_t)(w0 + g) * a.total_chunks + blockIdx.x] : 0;
-    vT[g] = g < nw ? h2f(okey_inv(T[g])) : 0.f;
   }
+  // phase A: every value's order key, and the rank of the values equal to T inside each wave
+  // (packed: key | rank in wave << 16 | equal << 23); one barrier for the whole block instead of two
+  // per (job slice, worker)
+  uint32_t pk[kJPT][kKG];
+  int32_t hbj[kJPT];
+  uint16_t cj[kJPT];
+  bool nob[kJPT];
+  const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
   for (int t = 0; t < kJPT; ++t) {
     const int64_t jj = t * 256 + threadIdx.x;
     const bool live = jj < ci.nj;
     const int64_t j = ci.j0 + jj;
-    const int32_t hbj = live ? a.hb[j] : -1;
-    const uint16_t cj = live ? a.cost[j] : 0;
-    const bool nob = live && a.nobid[j];
-    uint32_t best = 0;
-    for (int g = 0; g < nw; ++g) {
-      const int w = w0 + g;
-      const uint16_t vb = live ? value_bits(w, wrow(a, ci, w)[j], hbj, cj) : 0;
-      const uint32_t k = okey(vb);
-      const bool eq = live && k == T[g];
+    hbj[t] = live ? a.hb[j] : -1;
+    cj[t] = live ? a.cost[j] : 0;
+    nob[t] = live && a.nobid[j];
+    uint16_t v[kKG];
+#pragma unroll
+    for (int g = 0; g < kKG; ++g) v[g] = (g < nw && live) ? wrow(a, ci, w0 + g)[j] : 0;
+#pragma unroll
+    for (int g = 0; g < kKG; ++g) {
+      uint32_t k = 0;
+      if (g < nw && live) k = okey(value_bits(w0 + g, v[g], hbj[t], cj[t]));
+      const bool eq = g < nw && live && k == T[g];
       const unsigned long long m = __ballot(eq);
-      const uint32_t before_in_wave = __popcll(m & ((1ull << lane) - 1ull));
-      if (lane == 0) wsum[g][wv] = __popcll(m);
-      __syncthreads();
-      uint32_t before = off[g] + before_in_wave;
-      for (int q = 0; q < wv; ++q) before += wsum[g][q];
-      const uint32_t tot = wsum[g][0] + wsum[g][1] + wsum[g][2] + wsum[g][3];
-      __syncthreads();
-      off[g] += tot;
+      if (lane == 0) wcnt[t][g][wv] = __popcll(m);
+      pk[t][g] = k | ((uint32_t)__popcll(m & lt) << 16) | ((uint32_t)eq << 23) | ((uint32_t)live << 24);
+    }
+  }
+  __syncthreads();
+  // phase B: bids in job order (the tie rank of a job = equal values at lower jobs of the segment)
+  uint32_t best[kJPT] = {};
+#pragma unroll
+  for (int g = 0; g < kKG; ++g) {
+    const int w = w0 + g;
+    const float vT = h2f(okey_inv(T[g]));
+    uint32_t run = off[g];
+#pragma unroll
+    for (int t = 0; t < kJPT; ++t) {
+      const uint32_t c0 = wcnt[t][g][0], c1 = wcnt[t][g][1], c2 = wcnt[t][g][2], c3 = wcnt[t][g][3];
+      const uint32_t below = wv == 0 ? 0 : wv == 1 ? c0 : wv == 2 ? c0 + c1 : c0 + c1 + c2;
+      const uint32_t p = pk[t][g];
+      const uint32_t k = p & 0xFFFFu;
+      const bool eq = (p >> 23) & 1u, live = (p >> 24) & 1u;
+      const uint32_t before = run + below + ((p >> 16) & 63u);
+      run += c0 + c1 + c2 + c3;
       uint16_t bid = 0;
       if (live && k > T[g]) {
-        bid = f2h(h2f(f2h(h2f(vb) - vT[g])) + epsf);
+        bid = f2h(h2f(f2h(h2f(okey_inv(k)) - vT)) + epsf);
       } else if (eq && before < need[g]) {
         bid = f2h(0.0f + epsf);
       }
-      if (counter < 100 && hbj == w) bid = eps;        // retention bid of the previous winner
-      if (counter > 1000 && w == 0 && nob) bid = eps;  // leftovers go to worker 0
-      if (bid) best = max(best, ((uint32_t)bid << 16) | (0xFFFFu - (uint32_t)w));
+      if (counter < 100 && hbj[t] == w) bid = eps;        // retention bid of the previous winner
+      if (counter > 1000 && w == 0 && nob[t]) bid = eps;  // leftovers go to worker 0
+      if (bid && g < nw) best[t] = max(best[t], ((uint32_t)bid << 16) | (0xFFFFu - (uint32_t)w));
     }
-    if (best) atomicMax(&a.key[j], best);
   }
+#pragma unroll
+  for (int t = 0; t < kJPT; ++t)
+    if (best[t]) atomicMax(&a.key[ci.j0 + t * 256 + threadIdx.x], best[t]);
 }
 
 // ---- resolve: per job of the live segments, one block per chunk ----
