@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--traffic-json", default=str(REPO / "bench_data" / "traffic.json"),
                     help="PMC HBM bytes per launch of this build (tools/pmc_traffic.sh; shipped to the GPU box, "
                          "unlike profiles/); missing file -> traffic null")
+    ap.add_argument("--balanced-rows", type=int, default=1000000,
+                    help="rows of the balanced (auction) training iterations in 'train_balanced' (0 = skip)")
     ap.add_argument("--train-iters", type=int, default=3,
                     help="Lloyd iterations timed for the 'train' field (0 = skip)")
     ap.add_argument("--parity-rows", type=int, default=2048,
@@ -218,6 +220,52 @@ def train_iterations(x, c0, iters, world, n_global):
     return dt / iters * 1e3, n_global * iters / dt
 
 
+def balanced_iterations(x, cb, rows):
+    """The reference's actual training step is balanced: one iteration = fp16 scores
+    -distance + auction_lap_half + centroid update.  Times, on the first ``rows`` rows of this rank, one
+    level-0 iteration (K = 128, one auction) and one middle-layer iteration of all 128 parents in lockstep
+    (segments = the rows' level-0 parents, K = 128 each: rqsid_seg_auction_scores + rqsid_seg_auction_lap_half
+    + the update over 128 x 128 clusters), outside the encode's timed region."""
+    xs = x[:rows].contiguous()
+    c0 = torch.from_numpy(cb["c0"]).to(x.device).float()
+    c1 = torch.from_numpy(cb["c1"]).to(x.device).float()
+    k = c0.shape[0]
+
+    def level0():
+        w = ops.auction_scores(xs, c0, half=False)
+        a, r = ops.auction(w)
+        ops.centroid_update(xs, a, k, c0.clone())
+        return r
+
+    ids = ops.nearest(xs, ops.prepare_centers(c0))
+    xr = ops.residual(xs, c0, ids, normalize=True)
+    order = torch.sort(ids.long(), stable=True)[1]
+    sizes = torch.bincount(ids.long(), minlength=k).cpu().numpy()
+    xo = xr[order].contiguous()
+    lay = ops.SegmentLayout(sizes, x.device)
+    kk = c1.shape[0] // k
+
+    def middle():
+        w = ops.seg_auction_scores(xo, c1, kk, lay)
+        a, r = ops.seg_auction(w, kk, lay)
+        ops.centroid_update(xo, lay.seg_of_row * kk + a.long(), k * kk, c1.clone())
+        return int(r.max().item())
+
+    out = {}
+    for name, fn in (("level0", level0), ("middle_lockstep", middle)):
+        fn()  # warm-up
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        r = fn()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        out[name] = {"ms_per_iteration": round(dt * 1e3, 2), "auction_rounds": int(r), "rows": rows,
+                     "rows_per_s": round(rows / dt, 1)}
+    out["middle_lockstep"]["segments"] = int((sizes > 0).sum())
+    out["metric"] = "balanced Lloyd iteration (fp16 scores + auction_lap_half + centroid update)"
+    return out
+
+
 def check_sample(x, out, cb, rows):
     """The timed run's last output on an evenly spaced row sample vs the exact oracle (the checker only,
     after the timed region): the IDs must be identical."""
@@ -363,6 +411,8 @@ def main():
                                    + (", RCCL all_reduce of the [K*D+K] sums" if world > 1 else "") + ")",
                          "value": round(rps, 1), "unit": "rows/s", "ms_per_iteration": round(t_ms, 3),
                          "iterations": args.train_iters, "rows": n * world}
+    if args.balanced_rows > 0:
+        line["train_balanced"] = balanced_iterations(x, cb, min(args.balanced_rows, n))
     if args.parity_rows > 0:
         line["parity"] = check_sample(x, out, cb, args.parity_rows)
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
