@@ -47,7 +47,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rows", type=int, default=10_000_000, help="rows per GPU")
+    ap.add_argument("--preset", choices=("prod", "xl"), default="prod",
+                    help="prod: need [128,128,256], 2560 last-level candidates (BASELINE configs[2]/[3], the "
+                         "headline); xl: need [256,256,512], 5120 candidates (configs[4]: 50M rows over 8 GPUs = "
+                         "6.25M rows per GPU by default)")
+    ap.add_argument("--rows", type=int, default=0, help="rows per GPU (0: 10M for prod, 6.25M for xl)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="rows for the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--codebooks", choices=("fitted", "sampled"), default=os.environ.get("BENCH_CODEBOOKS", "fitted"),
@@ -61,7 +65,13 @@ def parse():
                     help="Lloyd iterations timed for the 'train' field (0 = skip)")
     ap.add_argument("--parity-rows", type=int, default=2048,
                     help="rows of the timed output checked against the exact CPU oracle after the run (0 = skip)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    global NEED, N_CAND
+    if a.preset == "xl":
+        NEED, N_CAND = [256, 256, 512], 5120
+    if a.rows <= 0:
+        a.rows = 6_250_000 if a.preset == "xl" else 10_000_000
+    return a
 
 
 # kernels of each encode level's rqsid_assign call (per-tile screen + exact re-score; see encode.py)
@@ -168,7 +178,7 @@ def fitted_codebooks(device, n_sample=1_000_000, seed=4321, iters=10):
 def codebooks(kind, device):
     if kind == "fitted":
         return fitted_codebooks(device)
-    return synth.encode_codebooks(seed=99)
+    return synth.encode_codebooks(seed=99, need=tuple(NEED), n_cand=N_CAND)
 
 
 def cpu_baseline(cb, rows):
@@ -362,7 +372,7 @@ def main():
         kern["bucket"] = {"ms": round(ms["bucket"], 3)}
     dom = max((k for k in kern if k.startswith("assign")), key=lambda k: kern[k]["ms"])
     dk = kern[dom]
-    traffic = level_traffic(args.traffic_json, int(dom[-1])) if os.environ.get("RQSID_SCREEN_VARIANT", "0") == "0" else None
+    traffic = level_traffic(args.traffic_json, int(dom[-1])) if os.environ.get("RQSID_SCREEN_VARIANT", "0") == "0" and NEED == [128, 128, 256] else None
     # Which roof applies: the level's algorithmic intensity (2 K_eff D flop per 2052 B: 64-128 flop/B) puts
     # its fp16 MFMA time at <= 6 % of its HBM time at the two peaks, so HBM is the roof; the PMC traffic
     # (when present) says whether the kernel moves more than its algorithmic bytes.
@@ -397,8 +407,9 @@ def main():
         "data": "synthetic Gaussian mixture (4096 blobs, sigma 0.25) generated on device; " +
                 ("PROD-shaped codebooks fitted on a 1M-row sample (short Lloyd fits, random init)" if args.codebooks == "fitted"
                  else "PROD-shaped codebooks sampled from residual rows"),
-        "config": {"workload": f"3-level RQ encode, {n} x {D} fp32 rows per GPU, need [128,128,256], "
-                               "layer_clusters [128,1280,1280] (BASELINE configs[2]/[3])",
+        "config": {"workload": f"3-level RQ encode, {n} x {D} fp32 rows per GPU, need {NEED}, layer_clusters "
+                               f"[{NEED[0]},{N_CAND // 2},{N_CAND // 2}] (BASELINE "
+                               + ("configs[2]/[3])" if NEED[0] == 128 else "configs[4] encode shapes)"),
                    "rows_per_gpu": n, "dim": D, "need_clusters": NEED, "candidates_last_level": N_CAND,
                    "parallelism": f"rows sharded x{world}, no collective",
                    "method": "fp16 MFMA screen (LDS-DMA ring) + fp64 re-score (exact argmin)"},

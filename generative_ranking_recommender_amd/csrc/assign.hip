@@ -1033,7 +1033,11 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   // (The 8-tile form has no 3-term build: its second accumulator set does not fit 256 VGPRs.)
   // ONE: single-pass segments take the collapsed-bound epilogue (RQSID_SCREEN_VARIANT=2: the
   // per-candidate two-sweep list epilogue, for comparison).
-  const bool t3 = cand_count_max <= 128 && (screen_terms == 3 || (screen_terms == 0 && res_levels >= 1));
+  // Wider first-residual levels (the XL preset's middle level: 256 candidates per parent) take the
+  // 3-term screen in two 128-candidate passes: the 1-term bound leaves ~2/3 of those rows to the fp64
+  // re-score (measured: 4.1 M of 6.25 M rows, 14.3 ms).
+  const bool t3 = (cand_count_max <= 128 && (screen_terms == 3 || (screen_terms == 0 && res_levels >= 1))) ||
+                  (cand_count_max <= 256 && (screen_terms == 3 || (screen_terms == 0 && res_levels == 1)));
   p.terms = t3 ? 3 : 1;
   const bool legacy = screen_variant() == 2;
   // the persistent streamed kernel (assign_stream.hip): 512-d rows, single-pass segments, no local-id
@@ -1081,7 +1085,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
     }
   }
   if (use_stream || use_res) {
-  } else if (t3) launch_screen2<4, 2, true>(p, res_levels, norm, grid, !legacy, st);
+  } else if (t3) launch_screen2<4, 2, true>(p, res_levels, norm, grid, !legacy && cand_count_max <= 128, st);
   else if (cand_count_max <= 128) launch_screen2<4, 2, false>(p, res_levels, norm, grid, !legacy, st);
   else if (cand_count_max <= 256) launch_screen2<8, 2, false>(p, res_levels, norm, grid, !legacy, st);
   else launch_screen<8, 2, false, false>(p, res_levels, norm, grid, st);

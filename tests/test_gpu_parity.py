@@ -122,7 +122,7 @@ def test_prepare_centers_table_scale():
 
 
 @pytest.mark.parametrize("terms", [1, 3])
-@pytest.mark.parametrize("k", [100, 128])
+@pytest.mark.parametrize("k", [100, 128, 200, 256])
 def test_screen_terms_same_ids(terms, k):
     """1- and 3-term screens return the same exact IDs (only the re-scored fraction differs)."""
     x = synth.small_mixture(6000, d=512, m=40, seed=k)
@@ -296,6 +296,28 @@ def test_encoder_full_size_properties():
     xs = x[torch.from_numpy(sel).to(DEV)].cpu().numpy()
     ref = O.encode(xs, [cb["c0"], cb["c1"], cb["c2"]], [128, 128, 256], cb["match"], residual_from_weighted=True,
                    exact=True)
+    assert (an[sel] == ref).all()
+
+
+def test_encoder_xl_shapes_properties():
+    """BASELINE configs[4] shapes (need [256,256,512], 5120 last-level candidates, 65536 groups): the
+    middle level screens 256 candidates per parent (1-term), the last level 512 per group (multi-pass
+    screen).  IDs in range, deterministic, fused == materialised, and a row sample identical to the
+    exact oracle."""
+    need = (256, 256, 512)
+    cb = synth.encode_codebooks(seed=5, need=need, n_cand=5120)
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], list(need),
+                    match=torch.from_numpy(cb["match"]), semantics=HIERARCHICAL_TRAIN, device=DEV)
+    x = gpu(synth.mixture_rows(0, 200000))
+    a = enc.encode(x)
+    assert torch.equal(a, enc.encode(x))
+    an = a.cpu().numpy()
+    assert an.min() >= 0 and (an.max(0) < np.array(need)).all()
+    enc.force_materialized = True
+    assert torch.equal(a, enc.encode(x))
+    sel = np.random.default_rng(2).choice(len(an), 2048, replace=False)
+    ref = O.encode(x[torch.from_numpy(sel).to(DEV)].cpu().numpy(), [cb["c0"], cb["c1"], cb["c2"]], list(need),
+                   cb["match"], residual_from_weighted=True, exact=True)
     assert (an[sel] == ref).all()
 
 
