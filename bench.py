@@ -230,7 +230,7 @@ def train_iterations(x, c0, iters, world, n_global):
     return dt / iters * 1e3, n_global * iters / dt
 
 
-def balanced_iterations(x, cb, rows):
+def balanced_iterations(x, cb, rows, world=1):
     """The reference's actual training step is balanced: one iteration = fp16 scores
     -distance + auction_lap_half + centroid update.  Times, on the first ``rows`` rows of this rank, one
     level-0 iteration (K = 128, one auction) and one middle-layer iteration of all 128 parents in lockstep
@@ -241,11 +241,26 @@ def balanced_iterations(x, cb, rows):
     c1 = torch.from_numpy(cb["c1"]).to(x.device).float()
     k = c0.shape[0]
 
-    def level0():
-        w = ops.auction_scores(xs, c0, half=False)
-        a, r = ops.auction(w)
-        ops.centroid_update(xs, a, k, c0.clone())
-        return r
+    if world > 1:
+        # row-sharded balanced step: the ranks' rows form one auction (distributed.ShardedAuction: two
+        # histogram all_reduces, one all_gather and one count all_reduce per round over RCCL) and the
+        # centroid sums one all_reduce
+        import torch.distributed as tdist
+        from generative_ranking_recommender_amd.distributed import GpuAuctionPasses, ShardedAuction
+
+        def level0():
+            w = ops.auction_scores(xs, c0, half=False)
+            a, r = ShardedAuction().run(GpuAuctionPasses(w, rows * world), rows * world, k)
+            sums, counts = ops.centroid_sums(xs, a.long(), k)
+            buf = torch.cat([sums.reshape(-1), counts.to(sums.dtype)])
+            tdist.all_reduce(buf)
+            return r
+    else:
+        def level0():
+            w = ops.auction_scores(xs, c0, half=False)
+            a, r = ops.auction(w)
+            ops.centroid_update(xs, a, k, c0.clone())
+            return r
 
     ids = ops.nearest(xs, ops.prepare_centers(c0))
     xr = ops.residual(xs, c0, ids, normalize=True)
@@ -269,9 +284,17 @@ def balanced_iterations(x, cb, rows):
         r = fn()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t
-        out[name] = {"ms_per_iteration": round(dt * 1e3, 2), "auction_rounds": int(r), "rows": rows,
-                     "rows_per_s": round(rows / dt, 1)}
+        if world > 1:
+            import torch.distributed as tdist
+            el = torch.tensor([dt], dtype=torch.float64, device=x.device)
+            tdist.all_reduce(el, op=tdist.ReduceOp.MAX)
+            dt = float(el.item())
+        tot = rows * (world if name == "level0" else 1)
+        out[name] = {"ms_per_iteration": round(dt * 1e3, 2), "auction_rounds": int(r), "rows": tot,
+                     "rows_per_s": round(tot / dt, 1)}
     out["middle_lockstep"]["segments"] = int((sizes > 0).sum())
+    out["level0"]["sharding"] = f"rows sharded x{world}, RCCL exchange per auction round" if world > 1 else "one GPU"
+    out["middle_lockstep"]["sharding"] = "per rank (rank 0's rows)"
     out["metric"] = "balanced Lloyd iteration (fp16 scores + auction_lap_half + centroid update)"
     return out
 
@@ -423,7 +446,10 @@ def main():
                          "value": round(rps, 1), "unit": "rows/s", "ms_per_iteration": round(t_ms, 3),
                          "iterations": args.train_iters, "rows": n * world}
     if args.balanced_rows > 0:
-        line["train_balanced"] = balanced_iterations(x, cb, min(args.balanced_rows, n))
+        try:
+            line["train_balanced"] = balanced_iterations(x, cb, min(args.balanced_rows, n), world)
+        except Exception as exc:  # a side measurement must not cost the encode line
+            line["train_balanced"] = {"error": repr(exc)[:300]}
     if args.parity_rows > 0:
         line["parity"] = check_sample(x, out, cb, args.parity_rows)
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:

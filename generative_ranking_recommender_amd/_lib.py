@@ -61,6 +61,16 @@ SIGNATURES = {
     "rqsid_seg_auction_workspace_bytes": (c_i64, [c_i64, c_i32, c_i32, c_i64, c_i32]),
     "rqsid_seg_auction_lap_half": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_i32, c_vp,
                                            c_vp, c_vp, c_i64, c_vp]),
+    "rqsid_dauction_workspace_bytes": (c_i64, [c_i64, c_i32]),
+    "rqsid_dauction_layout": (c_i32, [c_i64, c_i32, c_vp]),
+    "rqsid_dauction_begin": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "rqsid_dauction_eps": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    "rqsid_dauction_hist": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp]),
+    "rqsid_dauction_select": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp]),
+    "rqsid_dauction_eqcount": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    "rqsid_dauction_bid": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "rqsid_dauction_resolve": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "rqsid_dauction_end_round": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_i64, c_vp]),
     "rqsid_greedy_match": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "rqsid_mfma_probe": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }

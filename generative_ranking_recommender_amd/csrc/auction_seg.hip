@@ -65,6 +65,11 @@ struct SegAuction {
   uint32_t* hist;                // [n_multi*K][256]
   uint32_t* sel;                 // [S*K][4]: b1, rank in bin, T, need_eq
   uint32_t* eqcnt;               // [K][total_chunks]
+  // row-sharded mode (one segment spread over ranks, rqsid_dauction_*): the global job count decides
+  // jobs-per-worker and completion; rank_off[w] = equal-to-T values of worker w on lower ranks
+  int64_t n_glob;                // 0: single process
+  const uint32_t* rank_off;      // [K] or null
+  uint32_t* eqtot;               // [S*K] equal-to-T values per (segment, worker) on this rank
 };
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ off, int n_seg, int64_t i) {
@@ -109,12 +114,12 @@ __device__ __forceinline__ const uint16_t* wrow(const SegAuction& a, const Chunk
 __global__ __launch_bounds__(256) void sa_seg_init_kernel(SegAuction a, const uint8_t* __restrict__ active) {
   const int s = blockIdx.x * 256 + threadIdx.x;
   if (s >= a.S) return;
-  const int64_t n_s = a.seg_off[s + 1] - a.seg_off[s];
+  const int64_t n_s = a.n_glob ? a.n_glob : a.seg_off[s + 1] - a.seg_off[s];
   const int64_t nch = a.chunk_off[s + 1] - a.chunk_off[s];
   uint8_t f = 0;
   // live: requested, non-empty, and N_s >= K (N_s < K takes the argmin fallback, 0 rounds)
   if ((!active || active[s]) && n_s > 0 && n_s >= a.K) f |= kLive;
-  if (nch == 1) f |= kSingle;
+  if (nch == 1 && !a.n_glob) f |= kSingle;
   a.flag[s] = f;
   a.mm[2 * s] = 0;
   a.mm[2 * s + 1] = 0xFFFFFFFFu;
@@ -170,7 +175,8 @@ __global__ __launch_bounds__(256) void sa_eps_kernel(SegAuction a) {
 // N_s < K: the reference's argmin(-D) fallback (the FARTHEST centre), balancekmeans/__init__.py:24-26
 __global__ __launch_bounds__(256) void sa_fallback_kernel(SegAuction a, int32_t* __restrict__ out) {
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
-  if (ci.n_s >= a.K || ci.n_s == 0) return;
+  const int64_t n_dec = a.n_glob ? a.n_glob : ci.n_s;
+  if (n_dec >= a.K || ci.n_s == 0) return;
   for (int64_t t = threadIdx.x; t < ci.nj; t += 256) {
     const int64_t j = ci.j0 + t;
     float best = INFINITY;
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(256) void sa_select_kernel(SegAuction a) {
   const int s = a.mseg[hw / a.K];
   const int w = (int)(hw % a.K);
   if (!(a.flag[s] & kLive)) return;
-  const int64_t n_s = a.seg_off[s + 1] - a.seg_off[s];
+  const int64_t n_s = a.n_glob ? a.n_glob : a.seg_off[s + 1] - a.seg_off[s];
   const uint32_t jpw = (uint32_t)(n_s / a.K);
   uint32_t* h = a.hist + hw * 256;
   uint32_t* sel = a.sel + ((int64_t)s * a.K + w) * 4;
@@ -398,6 +404,7 @@ __global__ __launch_bounds__(256) void sa_eqscan_kernel(SegAuction a) {
     if (i < c1) e[i] = carry + x - v;
     carry += (uint32_t)__shfl((int)x, 63);
   }
+  if (lane == 0) a.eqtot[(int64_t)s * a.K + w] = carry;
 }
 
 // ---- bids: one packed {fp16 bid, ~worker} atomicMax per job and block ----
@@ -417,6 +424,7 @@ __global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a) {
     T[g] = g < nw ? a.sel[(sw0 + g) * 4 + 2] : 0xFFFFFFFFu;
     need[g] = g < nw ? a.sel[(sw0 + g) * 4 + 3] : 0;
     off[g] = (g < nw && !(f & kSingle)) ? a.eqcnt[(int64_t)(w0 + g) * a.total_chunks + blockIdx.x] : 0;
+    if (g < nw && a.rank_off) off[g] += a.rank_off[w0 + g];
   }
   // phase A: every value's order key, and the rank of the values equal to T inside each wave
   // (packed: key | rank in wave << 16 | equal << 23); one barrier for the whole block instead of two
@@ -515,7 +523,7 @@ __global__ __launch_bounds__(256) void sa_round_end_kernel(SegAuction a, int cou
   const int s = blockIdx.x * 256 + threadIdx.x;
   uint32_t live = 0;
   if (s < a.S && (a.flag[s] & kLive)) {
-    const int64_t n_s = a.seg_off[s + 1] - a.seg_off[s];
+    const int64_t n_s = a.n_glob ? a.n_glob : a.seg_off[s + 1] - a.seg_off[s];
     a.rounds[s] = round + 1;
     if ((int64_t)a.have[s] == n_s) a.flag[s] &= ~kLive;
     else live = 1;
@@ -534,7 +542,7 @@ __global__ __launch_bounds__(1024) void sa_multi_index_kernel(SegAuction a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int base = 0; base < a.S; base += 1024) {
     const int s = base + threadIdx.x;
-    const uint32_t v = (s < a.S && a.chunk_off[s + 1] - a.chunk_off[s] > 1) ? 1u : 0u;
+    const uint32_t v = (s < a.S && (a.chunk_off[s + 1] - a.chunk_off[s] > 1 || a.n_glob)) ? 1u : 0u;
     const unsigned long long m = __ballot(v);
     const uint32_t before = __popcll(m & ((1ull << lane) - 1ull));
     if (lane == 0) ws[wv] = __popcll(m);
@@ -585,6 +593,7 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.hist = c.take<uint32_t>((int64_t)a.n_multi * K * 256);
   a.sel = c.take<uint32_t>((int64_t)S * K * 4);
   a.eqcnt = c.take<uint32_t>((int64_t)K * total_chunks);
+  a.eqtot = c.take<uint32_t>((int64_t)S * K);
 }
 
 }  // namespace
@@ -730,6 +739,186 @@ int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_
   if (exec) (void)hipGraphExecDestroy(exec);
   (void)hipHostFree(host);
   return rc;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------------------
+// Row-sharded single auction, one pass per call (distributed.ShardedAuction drives the rounds and the
+// collectives between the passes).  The workspace holds a 512-B header (segment / chunk tables, round
+// count) and the segmented state with S = 1, every chunk on the global-histogram path.
+// ---------------------------------------------------------------------------------------------------------
+namespace {
+constexpr int64_t kDHeader = 512;
+
+__global__ void dauction_tables_kernel(int32_t* seg_off, int32_t* chunk_off, int32_t n, int32_t nch) {
+  seg_off[0] = 0;
+  seg_off[1] = n;
+  chunk_off[0] = 0;
+  chunk_off[1] = nch;
+}
+
+int dstate(SegAuction& a, const uint16_t* scores, int32_t k, int64_t n_local, int64_t n_global, void* ws,
+           int64_t wsb) {
+  if (!scores && n_local > 0) return fail(RQSID_E_ARG, "dauction: null scores");
+  if (k <= 1 || n_local < 0 || n_local > INT32_MAX || n_global < n_local || !ws)
+    return fail(RQSID_E_ARG, "dauction: bad arguments (K=%d n_local=%lld n_global=%lld)", k, (long long)n_local,
+                (long long)n_global);
+  const int64_t nch = cdiv(n_local, kCh);
+  a = SegAuction{};
+  a.W = scores;
+  a.K = k;
+  a.S = 1;
+  a.total_chunks = nch;
+  a.n_multi = 1;
+  a.n_glob = n_global > 0 ? n_global : 1;
+  char* p = (char*)ws;
+  a.seg_off = (const int32_t*)p;
+  a.chunk_off = (const int32_t*)(p + 64);
+  a.rounds = (int32_t*)(p + 128);
+  Carve c{p + kDHeader};
+  carve(a, c, n_local, k, 1, nch);
+  if (wsb < kDHeader + c.used) return fail(RQSID_E_WORKSPACE, "dauction: workspace too small");
+  return RQSID_OK;
+}
+
+int64_t dws(int64_t n_local, int32_t k) {
+  SegAuction a{};
+  a.n_multi = 1;
+  Carve c{nullptr};
+  carve(a, c, n_local, k, 1, cdiv(n_local, kCh));
+  return kDHeader + c.used;
+}
+}  // namespace
+
+extern "C" {
+
+int64_t rqsid_dauction_workspace_bytes(int64_t n_local, int32_t n_workers) {
+  if (n_local < 0 || n_workers <= 0) return -1;
+  return dws(n_local, n_workers);
+}
+
+int rqsid_dauction_layout(int64_t n_local, int32_t n_workers, int64_t* offsets) {
+  if (!offsets || n_local < 0 || n_workers <= 0) return fail(RQSID_E_ARG, "dauction_layout: bad arguments");
+  SegAuction a{};
+  a.n_multi = 1;
+  Carve c{(char*)nullptr + kDHeader};
+  carve(a, c, n_local, n_workers, 1, cdiv(n_local, kCh));
+  offsets[0] = (int64_t)((char*)a.mm - (char*)nullptr);     // u32 [2]: max key, min key
+  offsets[1] = (int64_t)((char*)a.hist - (char*)nullptr);   // u32 [K][256]
+  offsets[2] = (int64_t)((char*)a.eqtot - (char*)nullptr);  // u32 [K]
+  offsets[3] = (int64_t)((char*)a.have - (char*)nullptr);   // u32 [1]
+  return RQSID_OK;
+}
+
+int rqsid_dauction_begin(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                         int32_t* out_assign, void* workspace, int64_t workspace_bytes, void* stream) {
+  SegAuction a;
+  int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(dauction_tables_kernel, dim3(1), dim3(1), 0, st, (int32_t*)a.seg_off, (int32_t*)a.chunk_off,
+                     (int32_t)n_local, (int32_t)a.total_chunks);
+  hipLaunchKernelGGL(sa_seg_init_kernel, dim3(1), dim3(256), 0, st, a, (const uint8_t*)nullptr);
+  hipLaunchKernelGGL(sa_multi_index_kernel, dim3(1), dim3(1024), 0, st, a);
+  if (hipMemsetAsync(a.hist, 0, (size_t)n_workers * 256 * 4, st) != hipSuccess)
+    return fail(RQSID_E_LAUNCH, "dauction: memset");
+  if (n_local > 0) {
+    hipLaunchKernelGGL(sa_job_init_kernel, dim3(grid_cap(cdiv(n_local, 256), 8192)), dim3(256), 0, st, a, n_local);
+    hipLaunchKernelGGL(sa_fallback_kernel, dim3((unsigned)a.total_chunks), dim3(256), 0, st, a, out_assign);
+    hipLaunchKernelGGL(sa_minmax_kernel, dim3((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG)), dim3(256), 0,
+                       st, a);
+  }
+  return check_launch("dauction_begin");
+}
+
+// eps from the (caller-reduced) global min / max keys
+int rqsid_dauction_eps(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global, void* workspace,
+                       int64_t workspace_bytes, void* stream) {
+  SegAuction a;
+  int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
+  if (rc) return rc;
+  hipLaunchKernelGGL(sa_eps_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("dauction_eps");
+}
+
+// local histogram of the high (low = 0) or low (low = 1) byte of every worker's value keys
+int rqsid_dauction_hist(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global, int32_t low,
+                        void* workspace, int64_t workspace_bytes, void* stream) {
+  SegAuction a;
+  int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
+  if (rc) return rc;
+  if (n_local == 0) return RQSID_OK;
+  const dim3 g((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG));
+  if (low) hipLaunchKernelGGL((sa_hist_kernel<true>), g, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL((sa_hist_kernel<false>), g, dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("dauction_hist");
+}
+
+// selection from the (caller-reduced) histograms; clears them for the next pass
+int rqsid_dauction_select(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global, int32_t low,
+                          void* workspace, int64_t workspace_bytes, void* stream) {
+  SegAuction a;
+  int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
+  if (rc) return rc;
+  const unsigned g = (unsigned)cdiv(n_workers, 4);
+  if (low) hipLaunchKernelGGL((sa_select_kernel<true>), dim3(g), dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL((sa_select_kernel<false>), dim3(g), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("dauction_select");
+}
+
+// values equal to each worker's threshold: per-chunk offsets on this rank and the rank's totals (eqtot)
+int rqsid_dauction_eqcount(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                           void* workspace, int64_t workspace_bytes, void* stream) {
+  SegAuction a;
+  int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (n_local == 0) {
+    if (hipMemsetAsync(a.eqtot, 0, (size_t)n_workers * 4, st) != hipSuccess)
+      return fail(RQSID_E_LAUNCH, "dauction: memset");
+    return RQSID_OK;
+  }
+  hipLaunchKernelGGL(sa_eqcount_kernel, dim3((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG)), dim3(256), 0,
+                     st, a);
+  hipLaunchKernelGGL(sa_eqscan_kernel, dim3((unsigned)cdiv(n_workers, 4)), dim3(256), 0, st, a);
+  return check_launch("dauction_eqcount");
+}
+
+// bids of round `round` (rank_off[w]: equal-to-T values of worker w on lower ranks, device u32 [K])
+int rqsid_dauction_bid(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                       const uint32_t* rank_off, void* workspace, int64_t workspace_bytes, void* stream) {
+  SegAuction a;
+  int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
+  if (rc) return rc;
+  if (n_local == 0) return RQSID_OK;
+  a.rank_off = rank_off;
+  hipLaunchKernelGGL(sa_bid_kernel, dim3((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  return check_launch("dauction_bid");
+}
+
+// winners and costs of this rank's jobs; the rank's count of jobs with a bidder goes to `have`
+int rqsid_dauction_resolve(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                           int32_t* out_assign, void* workspace, int64_t workspace_bytes, void* stream) {
+  SegAuction a;
+  int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
+  if (rc) return rc;
+  if (n_local == 0) return RQSID_OK;
+  hipLaunchKernelGGL(sa_resolve_kernel, dim3((unsigned)a.total_chunks), dim3(256), 0, (hipStream_t)stream, a,
+                     out_assign);
+  return check_launch("dauction_resolve");
+}
+
+// end of a round, after the caller summed `have` over the ranks: done when it equals n_global
+int rqsid_dauction_end_round(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                             void* workspace, int64_t workspace_bytes, void* stream) {
+  SegAuction a;
+  int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
+  if (rc) return rc;
+  hipLaunchKernelGGL(sa_round_end_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, a, 0);
+  hipLaunchKernelGGL(sa_round_inc_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, a);
+  return check_launch("dauction_end_round");
 }
 
 }  // extern "C"

@@ -42,11 +42,13 @@ def _gpu_accumulate(x: torch.Tensor, a: torch.Tensor, k: int):
 
 
 class ShardedLloyd:
-    """Unbalanced K-Means (``KMeans.fit`` with balanced=False, balancekmeans/__init__.py:368-465) over
-    row shards.  ``x_local`` holds rows [start, stop) of the global matrix of ``n_global`` rows."""
+    """K-Means (``KMeans.fit``, balancekmeans/__init__.py:368-465) over row shards: unbalanced (nearest
+    centre) or, with ``balanced``, the reference's training assignment through a row-sharded auction
+    (ShardedAuction).  ``x_local`` holds rows [start, stop) of the global matrix of ``n_global`` rows."""
 
     def __init__(self, n_clusters: int, x_local: torch.Tensor, n_global: int, group=None,
-                 assign_fn: Optional[Callable] = None, accumulate_fn: Optional[Callable] = None):
+                 assign_fn: Optional[Callable] = None, accumulate_fn: Optional[Callable] = None,
+                 balanced: bool = False, half: bool = False):
         self.k = n_clusters
         self.x = x_local
         self.n = n_global
@@ -56,7 +58,10 @@ class ShardedLloyd:
         self.start, self.stop = shard_bounds(n_global, self.rank, self.world)
         if x_local.shape[0] != self.stop - self.start:
             raise ValueError(f"rank {self.rank}: expected rows [{self.start}, {self.stop}) of {n_global}")
-        self.assign_fn = assign_fn or _gpu_assign
+        if assign_fn is None:
+            # balanced (KMeans(balanced=True), the reference's training): the row-sharded auction
+            assign_fn = (lambda x, c: sharded_balanced_assign(x, c, n_global, half, group)) if balanced else _gpu_assign
+        self.assign_fn = assign_fn
         self.accumulate_fn = accumulate_fn or _gpu_accumulate
         self.cluster_centers = None
 
@@ -104,3 +109,147 @@ class ShardedLloyd:
                 break
         self.cluster_centers = centers
         return a
+
+
+# ----------------------------------------------------------------------------------------------------
+# Row-sharded balanced assignment (SURVEY.md §8e "auction rebalance": one exchange per round)
+# ----------------------------------------------------------------------------------------------------
+class GpuAuctionPasses:
+    """The passes of one rank's share of an auction_lap_half (include/rqsid.h rqsid_dauction_*) on its
+    worker-major fp16 scores [K][n_local]; the buffers the driver reduces are views into the workspace."""
+
+    def __init__(self, scores_wj: torch.Tensor, n_global: int):
+        import ctypes
+        self.w = scores_wj.to(torch.float16).contiguous()
+        ops._require_device(self.w)
+        self.k, self.n_local = self.w.shape
+        self.n_global = int(n_global)
+        lib = ops.lib()
+        self.lib = lib
+        self.wsb = int(lib.rqsid_dauction_workspace_bytes(self.n_local, self.k))
+        self.ws = torch.zeros(self.wsb, dtype=torch.uint8, device=self.w.device)
+        offs = (ctypes.c_int64 * 4)()
+        ops._lib.check(lib.rqsid_dauction_layout(self.n_local, self.k, offs), "rqsid_dauction_layout")
+        k = self.k
+        self._mm = self.ws[offs[0]:offs[0] + 8].view(torch.int32)
+        self._hist = self.ws[offs[1]:offs[1] + k * 256 * 4].view(torch.int32).view(k, 256)
+        self._eqtot = self.ws[offs[2]:offs[2] + k * 4].view(torch.int32)
+        self._have = self.ws[offs[3]:offs[3] + 4].view(torch.int32)
+        self.out = torch.full((max(self.n_local, 1),), -1, dtype=torch.int32, device=self.w.device)
+
+    def _args(self):
+        return (ops._ptr(self.w) if self.n_local else None, self.k, self.n_local, self.n_global)
+
+    def _tail(self):
+        return (ops._ptr(self.ws), self.wsb, ops._stream())
+
+    def begin(self) -> torch.Tensor:
+        ops._lib.check(self.lib.rqsid_dauction_begin(*self._args(), ops._ptr(self.out), *self._tail()),
+                       "rqsid_dauction_begin")
+        return self._mm.to(torch.int64) & 0xFFFFFFFF  # {max key, min key} of this rank's scores
+
+    def set_minmax(self, mx: int, mn: int) -> None:
+        self._mm.copy_(torch.tensor([mx, mn], dtype=torch.int64).to(torch.int32))
+        ops._lib.check(self.lib.rqsid_dauction_eps(*self._args(), *self._tail()), "rqsid_dauction_eps")
+
+    def hist(self, low: int) -> torch.Tensor:
+        ops._lib.check(self.lib.rqsid_dauction_hist(*self._args(), int(low), *self._tail()), "rqsid_dauction_hist")
+        return self._hist
+
+    def select(self, low: int) -> None:
+        ops._lib.check(self.lib.rqsid_dauction_select(*self._args(), int(low), *self._tail()),
+                       "rqsid_dauction_select")
+
+    def eqcount(self) -> torch.Tensor:
+        ops._lib.check(self.lib.rqsid_dauction_eqcount(*self._args(), *self._tail()), "rqsid_dauction_eqcount")
+        return self._eqtot
+
+    def bid(self, rank_off: torch.Tensor) -> None:
+        ro = rank_off.to(torch.int32).to(self.w.device).contiguous()
+        ops._lib.check(self.lib.rqsid_dauction_bid(*self._args(), ops._ptr(ro), *self._tail()), "rqsid_dauction_bid")
+
+    def resolve(self) -> torch.Tensor:
+        ops._lib.check(self.lib.rqsid_dauction_resolve(*self._args(), ops._ptr(self.out), *self._tail()),
+                       "rqsid_dauction_resolve")
+        return self._have
+
+    def end_round(self) -> None:
+        ops._lib.check(self.lib.rqsid_dauction_end_round(*self._args(), *self._tail()), "rqsid_dauction_end_round")
+
+    def result(self) -> torch.Tensor:
+        return self.out[:self.n_local]
+
+
+class ShardedAuction:
+    """auction_lap_half (balancekmeans/__init__.py:12-140) over jobs split in contiguous blocks across the
+    ranks of ``group`` (rank r's block follows rank r-1's).  Per round: the two radix histograms of every
+    worker's values are summed over the ranks (2 x all_reduce of K*256 int32), the counts of values equal
+    to each worker's threshold are all-gathered (each rank's tie ranks start after the lower ranks'), and
+    the count of jobs with a bidder is summed (all_reduce of one int32).  Every rank ends each round with
+    identical thresholds and the same stop decision, and the assignment equals the single-process auction
+    of the whole matrix (same fp16 operations, same tie rule)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        # gloo (the CPU test backend) stages device tensors through host memory; RCCL reduces in place
+        self.stage = dist.get_backend(group) == "gloo"
+
+    def _all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> None:
+        if self.stage and t.is_cuda:
+            h = t.cpu()
+            dist.all_reduce(h, op=op, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op, group=self.group)
+
+    def _all_gather(self, t: torch.Tensor):
+        src = t.cpu() if self.stage and t.is_cuda else t.contiguous()
+        parts = [torch.zeros_like(src) for _ in range(self.world)]
+        dist.all_gather(parts, src, group=self.group)
+        return [p.to(t.device) for p in parts]
+
+    def run(self, passes, n_global: int, k: int, max_rounds: int = 0):
+        """Returns (this rank's assignment, rounds run)."""
+        if n_global == 0:
+            return passes.result(), 0
+        if k == 1:
+            raise ValueError("auction: a single worker cannot bid on N + 1 jobs")
+        mm = passes.begin()
+        if n_global < k:  # the reference's argmin(-D) fallback, per job (begin wrote it)
+            return passes.result(), 0
+        mx, mn = mm[0:1].clone(), mm[1:2].clone()
+        self._all_reduce(mx, dist.ReduceOp.MAX)
+        self._all_reduce(mn, dist.ReduceOp.MIN)
+        passes.set_minmax(int(mx.item()), int(mn.item()))
+        rounds = 0
+        while True:
+            for low in (0, 1):
+                h = passes.hist(low)
+                self._all_reduce(h)
+                passes.select(low)
+            e = passes.eqcount()
+            parts = self._all_gather(e)
+            rank_off = torch.zeros_like(e)
+            for r in range(self.rank):
+                rank_off += parts[r]
+            passes.bid(rank_off)
+            have = passes.resolve()
+            self._all_reduce(have)
+            done = int(have.item()) == n_global  # read before end_round clears the counter
+            passes.end_round()
+            rounds += 1
+            if done:
+                return passes.result(), rounds
+            if max_rounds and rounds >= max_rounds:
+                raise RuntimeError(f"auction: no complete assignment after {max_rounds} rounds")
+
+
+def sharded_balanced_assign(x_local: torch.Tensor, centers: torch.Tensor, n_global: int, half: bool = False,
+                            group=None) -> torch.Tensor:
+    """auction_lap_half(-pairwise_distance(X, C)) with X row-sharded: each rank scores its rows against all
+    centres (rqsid_auction_scores) and the ranks run one ShardedAuction.  Returns this rank's worker ids."""
+    w = ops.auction_scores(x_local.contiguous(), centers.float().contiguous(), half=half)
+    a, _ = ShardedAuction(group).run(GpuAuctionPasses(w, n_global), n_global, centers.shape[0])
+    return a.long()

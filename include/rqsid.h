@@ -207,6 +207,37 @@ int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_
                                int32_t* out_assign, int32_t* out_rounds, void* workspace,
                                int64_t workspace_bytes, void* stream);
 
+/* Row-sharded balanced assignment, one pass per call: the auction_lap_half of balancekmeans/__init__.py:
+ * 12-140 over jobs spread across ranks (rank r owns a contiguous block of n_local of the n_global jobs,
+ * scores [k][n_local] fp16 worker-major).  The caller (distributed.ShardedAuction) runs, per round,
+ * hist(0) -> sum the [k][256] u32 histograms over ranks -> select(0) -> hist(1) -> sum -> select(1) ->
+ * eqcount -> rank_off[w] = eqtot[w] summed over lower ranks -> bid(rank_off) -> resolve -> sum `have`
+ * over ranks -> end_round, and stops when the summed `have` equals n_global; after begin it reduces the
+ * {max, min} order keys (max / min over ranks) and calls eps.  Every fp16 operation and the tie rule
+ * (lowest GLOBAL job index at the top-k boundary, lowest worker among equal bids) are those of
+ * rqsid_auction_lap_half, so the assignment equals the single-process auction of the whole matrix.
+ * rqsid_dauction_layout gives the byte offsets, inside the workspace, of the buffers the caller
+ * reduces: [0] u32[2] {max key, min key} (min initialised to 0xFFFFFFFF), [1] u32 [k][256] histogram,
+ * [2] u32 [k] eqtot, [3] u32 have. */
+int64_t rqsid_dauction_workspace_bytes(int64_t n_local, int32_t n_workers);
+int rqsid_dauction_layout(int64_t n_local, int32_t n_workers, int64_t* offsets);
+int rqsid_dauction_begin(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                         int32_t* out_assign, void* workspace, int64_t workspace_bytes, void* stream);
+int rqsid_dauction_eps(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                       void* workspace, int64_t workspace_bytes, void* stream);
+int rqsid_dauction_hist(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                        int32_t low, void* workspace, int64_t workspace_bytes, void* stream);
+int rqsid_dauction_select(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                          int32_t low, void* workspace, int64_t workspace_bytes, void* stream);
+int rqsid_dauction_eqcount(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                           void* workspace, int64_t workspace_bytes, void* stream);
+int rqsid_dauction_bid(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                       const uint32_t* rank_off, void* workspace, int64_t workspace_bytes, void* stream);
+int rqsid_dauction_resolve(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                           int32_t* out_assign, void* workspace, int64_t workspace_bytes, void* stream);
+int rqsid_dauction_end_round(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                             void* workspace, int64_t workspace_bytes, void* stream);
+
 /* Greedy unique-nearest match rows (_assign_last_match_matrix hierarchical_rq_kmeans.py:1022-1038,
  * _get_dynamic_match_matrix simplified_semantic_id_generator.py:282-291): group g owns rows
  * sub_off[g]..sub_off[g+1] of dist [total][n_cand]; its first min(rows, max_take) rows each take, in

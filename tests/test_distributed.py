@@ -82,3 +82,168 @@ def test_shard_bounds_cover_rows():
             spans = [shard_bounds(n, r, w) for r in range(w)]
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+
+
+# ---- row-sharded auction: the driver's collective protocol with a numpy restatement of the passes ----
+F32 = np.float32
+
+
+def _okey(b):
+    """16-bit order key of fp16 bit patterns (larger value <-> larger key, -0 == +0), as the kernels."""
+    b = b.astype(np.uint32)
+    b = np.where(b == 0x8000, 0, b)
+    return np.where(b & 0x8000, (~b) & 0xFFFF, b | 0x8000).astype(np.uint32)
+
+
+def _okey_inv(k):
+    k = np.asarray(k, dtype=np.uint32)
+    return np.where(k & 0x8000, k & 0x7FFF, (~k) & 0xFFFF).astype(np.uint16)
+
+
+def _h(bits):
+    return np.asarray(bits, dtype=np.uint16).view(np.float16).astype(F32)
+
+
+class NumpyAuctionPasses:
+    """The per-pass steps of auction_seg.hip restated on numpy (test stand-in for GpuAuctionPasses)."""
+
+    def __init__(self, w16, n_global):
+        self.w = np.ascontiguousarray(w16.astype(np.float16))
+        self.k, self.n = self.w.shape
+        self.n_global = n_global
+        self.cost = np.zeros(self.n, np.float16)
+        self.hb = np.full(self.n, -1)
+        self.nobid = np.zeros(self.n, bool)
+        self.out = np.full(self.n, -1)
+        self.round = 0
+        self.jpw = n_global // self.k
+
+    def _keys(self):
+        v = (self.w.astype(F32) - self.cost[None, :].astype(F32)).astype(np.float16)
+        own = self.hb[None, :] == np.arange(self.k)[:, None]
+        v = np.where(own, self.w, v)
+        return _okey(v.view(np.uint16))
+
+    def begin(self):
+        if self.n_global < self.k:
+            self.out = self.w.astype(F32).argmin(0)
+        if self.n == 0:
+            return torch.tensor([0, 0xFFFFFFFF], dtype=torch.int64)
+        key = _okey(self.w.view(np.uint16))
+        return torch.tensor([int(key.max()), int(key.min())], dtype=torch.int64)
+
+    def set_minmax(self, mx, mn):
+        spread = np.float16(_h(_okey_inv(mx)) - _h(_okey_inv(mn)))
+        eps = np.float16(F32(spread) / F32(50.0))
+        self.eps = eps if eps >= np.float16(1e-4) else np.float16(1e-4)
+
+    def hist(self, low):
+        key = self._keys()
+        h = np.zeros((self.k, 256), np.int32)
+        for w in range(self.k):
+            kw = key[w]
+            if low:
+                kw = kw[(kw >> 8) == self.b1[w]] & 255
+            else:
+                kw = kw >> 8
+            np.add.at(h[w], kw, 1)
+        self.h = torch.from_numpy(h)
+        return self.h
+
+    def select(self, low):
+        h = self.h.numpy()
+        if not low:
+            self.b1, self.rk, self.ab1 = np.zeros(self.k, int), np.zeros(self.k, int), np.zeros(self.k, int)
+        else:
+            self.T, self.need = np.zeros(self.k, np.uint32), np.zeros(self.k, int)
+        for w in range(self.k):
+            rank = self.jpw + 1 if not low else self.rk[w]
+            above, b = 0, 255
+            while b > 0 and above + h[w, b] < rank:
+                above += h[w, b]
+                b -= 1
+            if not low:
+                self.b1[w], self.rk[w], self.ab1[w] = b, rank - above, above
+            else:
+                self.T[w] = (self.b1[w] << 8) | b
+                self.need[w] = self.jpw - (self.ab1[w] + above)
+
+    def eqcount(self):
+        self.key = self._keys()
+        return torch.from_numpy((self.key == self.T[:, None]).sum(1).astype(np.int32))
+
+    def bid(self, rank_off):
+        key, ro = self.key, rank_off.numpy()
+        best = np.zeros(self.n, np.uint32)
+        for w in range(self.k):
+            eq = key[w] == self.T[w]
+            before = ro[w] + np.cumsum(eq) - eq
+            vT = _h(_okey_inv(self.T[w]))
+            bid = np.zeros(self.n, np.float16)
+            gt = key[w] > self.T[w]
+            bid[gt] = (np.float16(_h(_okey_inv(key[w][gt])) - vT).astype(F32) + F32(self.eps)).astype(np.float16)
+            tie = eq & (before < self.need[w])
+            bid[tie] = np.float16(F32(0) + F32(self.eps))
+            if self.round < 100:
+                bid[self.hb == w] = self.eps
+            if self.round > 1000 and w == 0:
+                bid[self.nobid] = self.eps
+            pk = (bid.view(np.uint16).astype(np.uint32) << 16) | np.uint32(0xFFFF - w)
+            best = np.where(bid.view(np.uint16) != 0, np.maximum(best, pk), best)
+        self.best = best
+
+    def resolve(self):
+        k = self.best
+        won = k != 0
+        w = (0xFFFF - (k & 0xFFFF)).astype(np.int64)
+        bidv = (k >> 16).astype(np.uint16).view(np.float16)
+        self.out = np.where(won, w, -1)
+        self.hb = self.out.copy()
+        self.nobid = ~won
+        self.cost = np.where(won, (self.cost.astype(F32) + bidv.astype(F32)).astype(np.float16), self.cost)
+        return torch.tensor([int(won.sum())], dtype=torch.int32)
+
+    def end_round(self):
+        self.round += 1
+
+    def result(self):
+        return torch.from_numpy(np.asarray(self.out, dtype=np.int64))
+
+
+def _auction_worker(rank, world, port, w16, out):
+    from generative_ranking_recommender_amd.distributed import ShardedAuction
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = w16.shape[1]
+    s, e = shard_bounds(n, rank, world)
+    a, rounds = ShardedAuction().run(NumpyAuctionPasses(w16[:, s:e], n), n, w16.shape[0], max_rounds=1100)
+    width = -(-n // world)
+    pad = torch.full((width,), -1, dtype=torch.int64)
+    pad[: e - s] = a
+    gathered = [torch.zeros(width, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(gathered, pad)
+    if rank == 0:
+        full = torch.cat([g[: shard_bounds(n, r, world)[1] - shard_bounds(n, r, world)[0]]
+                          for r, g in enumerate(gathered)])
+        out.put((full.numpy(), rounds))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,k,levels", [(2, 64, 8, 3), (2, 67, 8, 4), (3, 200, 16, 50), (2, 5, 8, 3)])
+def test_sharded_auction_matches_single_process(world, n, k, levels):
+    """Row-sharded auction (world 2/3, gloo) == the single-process stable-tie oracle on the whole matrix,
+    including heavy ties across the shard boundary, N % K != 0 (1002 rounds) and N < K (fallback)."""
+    rng = np.random.default_rng(n + k)
+    w16 = (-rng.integers(1, levels + 1, size=(k, n)).astype(F32) * F32(0.37)).astype(np.float16)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_auction_worker, args=(r, world, port, w16, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, rounds = q.get(timeout=600)
+    for p in procs:
+        p.join(60)
+    want = O.auction_lap_half(w16.T.astype(F32), tie_rule="stable")
+    assert np.array_equal(got, want)
+    assert rounds >= (1 if n >= k else 0)

@@ -219,3 +219,69 @@ def test_greedy_match_matches_numpy(n_cand):
             want[g, c] = 1
     assert (got == want).all()
     assert (nsel.cpu().numpy() == want.sum(1)).all()
+
+
+def _gpu_sharded_auction_worker(rank, world, port, w16, out):
+    import os
+    import torch.distributed as dist
+    from generative_ranking_recommender_amd.distributed import GpuAuctionPasses, ShardedAuction, shard_bounds
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = w16.shape[1]
+    s, e = shard_bounds(n, rank, world)
+    try:
+        w = torch.from_numpy(np.ascontiguousarray(w16[:, s:e])).to(DEV)
+        a, rounds = ShardedAuction().run(GpuAuctionPasses(w, n), n, w16.shape[0], max_rounds=1100)
+        out.put((rank, a.cpu().numpy().astype(np.int64), rounds))
+    except Exception as exc:  # report instead of leaving the parent waiting
+        out.put((rank, None, repr(exc)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,k,levels", [(3000, 16, 7), (640, 64, 1000)])
+def test_sharded_auction_gpu_passes_two_ranks(n, k, levels):
+    """Two ranks on one GPU (gloo collectives over device tensors), each running the rqsid_dauction_*
+    passes on its row block: the concatenation equals the single-process GPU auction (pinned to the
+    oracle above), ties across the shard boundary included."""
+    import socket
+    import torch.multiprocessing as mp
+    rng = np.random.default_rng(n)
+    w16 = (-rng.integers(1, levels + 1, size=(k, n)).astype(np.float32) * np.float32(0.37)).astype(np.float16)
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gpu_sharded_auction_worker, args=(r, 2, port, w16, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=150) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+    assert all(r[1] is not None for r in res), res
+    got = np.concatenate([r[1] for r in res])
+    want, r_want = ops.auction(torch.from_numpy(w16).to(DEV))
+    assert np.array_equal(got, want.cpu().numpy())
+    assert res[0][2] == res[1][2] == r_want
+
+
+def test_sharded_balanced_fit_world1(tmp_path):
+    """ShardedLloyd(balanced=True) over RCCL with one rank == KMeans(balanced=True).fit (same draws)."""
+    import torch.distributed as dist
+    from generative_ranking_recommender_amd.distributed import ShardedLloyd
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1)
+    try:
+        x = torch.from_numpy(synth.small_mixture(3000, m=20, seed=2)).to(DEV)
+        seeded(5)
+        sl = ShardedLloyd(24, x, len(x), balanced=True)
+        a = sl.fit(iter_limit=3)
+        seeded(5)
+        km = KMeans(n_clusters=24, device=DEV, balanced=True)
+        a_ref = km.fit(x, iter_limit=3)
+        assert (a.cpu() == a_ref).all()
+        torch.testing.assert_close(sl.cluster_centers, km.cluster_centers, rtol=1e-6, atol=1e-6)
+    finally:
+        dist.destroy_process_group()
