@@ -7,7 +7,7 @@ set -u
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-traffic}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS="--steps 2 --warmup 1 --no-cpu ${BENCH_ARGS:-}"
+ARGS="--steps 2 --warmup 1 --no-cpu --balanced-rows 0 --train-iters 0 --parity-rows 0 ${BENCH_ARGS:-}"
 i=0
 for c in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
