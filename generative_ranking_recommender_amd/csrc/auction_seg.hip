@@ -26,6 +26,7 @@ namespace {
 constexpr int kKG = 16;        // workers per block
 constexpr int kCh = 1024;      // jobs per chunk
 constexpr int kJPT = kCh / 256;
+static_assert(kJPT * kKG == 64, "sa_bid_kernel keeps one deferral bit per (job slice, worker) in a u64");
 
 __device__ __forceinline__ float h2f(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
 __device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
@@ -106,8 +107,37 @@ __device__ __forceinline__ uint16_t value_bits(int w, uint16_t wv, int32_t hbj, 
   return f2h(h2f(wv) - h2f(cj));
 }
 
+// the same value as fp16: every step of the reference is one fp16 rounding of an fp32 result of two fp16
+// operands, which equals the fp16 operation itself (11-bit operands, 24-bit intermediate: the double
+// rounding is innocuous); order and equality of these values are those of okey (-0 == +0, no NaN)
+__device__ __forceinline__ _Float16 value_h(int w, uint16_t wv, int32_t hbj, uint16_t cj) {
+  const _Float16 r = __builtin_bit_cast(_Float16, wv);
+  return hbj == w ? r : (_Float16)(r - __builtin_bit_cast(_Float16, cj));
+}
+
 __device__ __forceinline__ const uint16_t* wrow(const SegAuction& a, const ChunkInfo& ci, int w) {
   return a.W + (int64_t)a.K * ci.seg_j0 + (int64_t)w * ci.n_s - ci.seg_j0;  // index with the global job
+}
+
+// One chunk's scores for the block's workers, with the jobs' winners and costs: every load is
+// unconditional (the job and worker indices are clamped into the segment), so the compiler issues the
+// whole chunk's loads at once and counts them, instead of draining the queue at each conditional load.
+// Lanes past the chunk's end (t * 256 + lane >= nj) hold copies and must be masked with `live`.
+struct ChunkScores {
+  uint16_t v[kJPT][kKG];
+  int32_t hb[kJPT];
+  uint16_t c[kJPT];
+};
+
+__device__ __forceinline__ void load_chunk(const SegAuction& a, const ChunkInfo& ci, int w0, ChunkScores& cs) {
+#pragma unroll
+  for (int t = 0; t < kJPT; ++t) {
+    const int64_t j = ci.j0 + min((int64_t)(t * 256 + threadIdx.x), ci.nj - 1);
+    cs.hb[t] = a.hb[j];
+    cs.c[t] = a.cost[j];
+#pragma unroll
+    for (int g = 0; g < kKG; ++g) cs.v[t][g] = wrow(a, ci, min(w0 + g, a.K - 1))[j];
+  }
 }
 
 // ---- setup ----
@@ -230,28 +260,40 @@ __global__ __launch_bounds__(256) void sa_hist_kernel(SegAuction a) {
   if (!(f & kLive) || (f & kSingle)) return;
   __shared__ uint32_t h[kKG][256];
   const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
+  const int lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < kKG * 256; i += 256) (&h[0][0])[i] = 0;
   __syncthreads();
   const int64_t sw0 = (int64_t)ci.s * a.K + w0;
   const int64_t hw0 = (int64_t)a.hidx[ci.s] * a.K + w0;
-  uint32_t b1[kKG];
-  if (LOW)
-    for (int g = 0; g < kKG; ++g) b1[g] = g < nw ? a.sel[(sw0 + g) * 4 + 0] : 0;
-  for (int t = 0; t < kJPT; ++t) {
-    const int64_t jj = t * 256 + threadIdx.x;
-    if (jj >= ci.nj) break;
-    const int64_t j = ci.j0 + jj;
-    const int32_t hbj = a.hb[j];
-    const uint16_t cj = a.cost[j];
-    uint16_t v[kKG];
+  // high-byte pass: a worker's values crowd into one or two high-byte bins, where same-address LDS
+  // atomics serialise a wave 64-fold.  The bins at and just below last round's threshold (sel[0]; any
+  // value is correct, it only decides which bins take the fast path) are counted with ballots.
+  // low-byte pass: only the values in the selected bin b1 count.
+  uint32_t b1[kKG], n0[kKG] = {}, n1[kKG] = {};
+  for (int g = 0; g < kKG; ++g) b1[g] = g < nw ? a.sel[(sw0 + g) * 4 + 0] & 255u : 0;
+  ChunkScores cs;
+  load_chunk(a, ci, w0, cs);
 #pragma unroll
-    for (int g = 0; g < kKG; ++g) v[g] = g < nw ? wrow(a, ci, w0 + g)[j] : 0;  // all loads in flight first
+  for (int t = 0; t < kJPT; ++t) {
+    const bool live = t * 256 + (int)threadIdx.x < ci.nj;
 #pragma unroll
     for (int g = 0; g < kKG; ++g) {
       if (g >= nw) continue;
-      const uint32_t k = okey(value_bits(w0 + g, v[g], hbj, cj));
-      if (!LOW) atomicAdd(&h[g][k >> 8], 1u);
-      else if ((k >> 8) == b1[g]) atomicAdd(&h[g][k & 255], 1u);
+      const uint32_t k = okey(value_bits(w0 + g, cs.v[t][g], cs.hb[t], cs.c[t]));
+      if (LOW) {
+        if (live && (k >> 8) == b1[g]) atomicAdd(&h[g][k & 255], 1u);
+      } else {
+        const uint32_t d = b1[g] - (k >> 8);  // 0: the guessed bin, 1: the bin below
+        n0[g] += (uint32_t)__popcll(__ballot(live && d == 0));
+        n1[g] += (uint32_t)__popcll(__ballot(live && d == 1));
+        if (live && d > 1) atomicAdd(&h[g][k >> 8], 1u);
+      }
+    }
+  }
+  if (!LOW && lane == 0) {
+    for (int g = 0; g < nw; ++g) {
+      if (n0[g]) atomicAdd(&h[g][b1[g]], n0[g]);
+      if (n1[g]) atomicAdd(&h[g][b1[g] - 1], n1[g]);  // n1 > 0 implies b1 >= 1
     }
   }
   __syncthreads();
@@ -357,21 +399,18 @@ __global__ __launch_bounds__(256) void sa_eqcount_kernel(SegAuction a) {
   const int64_t sw0 = (int64_t)ci.s * a.K + w0;
   if (threadIdx.x < kKG) c[threadIdx.x] = 0;
   __syncthreads();
-  uint32_t T[kKG];
-  for (int g = 0; g < kKG; ++g) T[g] = g < nw ? a.sel[(sw0 + g) * 4 + 2] : 0xFFFFFFFFu;
+  _Float16 vT[kKG];
+  for (int g = 0; g < kKG; ++g)
+    vT[g] = __builtin_bit_cast(_Float16, g < nw ? okey_inv(a.sel[(sw0 + g) * 4 + 2]) : (uint16_t)0);
   uint32_t cnt[kKG] = {};
-  for (int t = 0; t < kJPT; ++t) {
-    const int64_t jj = t * 256 + threadIdx.x;
-    if (jj >= ci.nj) break;
-    const int64_t j = ci.j0 + jj;
-    const int32_t hbj = a.hb[j];
-    const uint16_t cj = a.cost[j];
-    uint16_t v[kKG];
+  ChunkScores cs;
+  load_chunk(a, ci, w0, cs);
 #pragma unroll
-    for (int g = 0; g < kKG; ++g) v[g] = g < nw ? wrow(a, ci, w0 + g)[j] : 0;
+  for (int t = 0; t < kJPT; ++t) {
+    const bool live = t * 256 + (int)threadIdx.x < ci.nj;
 #pragma unroll
     for (int g = 0; g < kKG; ++g)
-      if (g < nw) cnt[g] += okey(value_bits(w0 + g, v[g], hbj, cj)) == T[g];
+      if (g < nw) cnt[g] += live && value_h(w0 + g, cs.v[t][g], cs.hb[t], cs.c[t]) == vT[g];
   }
   for (int g = 0; g < nw; ++g) {
     uint32_t v = cnt[g];
@@ -408,79 +447,78 @@ __global__ __launch_bounds__(256) void sa_eqscan_kernel(SegAuction a) {
 }
 
 // ---- bids: one packed {fp16 bid, ~worker} atomicMax per job and block ----
+// Phase A settles every value that does not need its tie rank (above T, below T, the retention and
+// leftover overrides) in one pass in fp16 and records each wave's ballot of the values equal to T.
+// Phase B visits only the (job slice, worker) pairs where some lane holds an equal value whose bid
+// depends on its rank among the segment's equal values in job order.
 __global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a) {
   const int counter = *a.round_dev;
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
   if (!(f & kLive)) return;
-  __shared__ uint32_t wcnt[kJPT][kKG][4];  // per (job slice, worker, wave): values equal to T
+  __shared__ unsigned long long eqm[kJPT][kKG][4];  // per (job slice, worker, wave): values equal to T
   const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
   const int64_t sw0 = (int64_t)ci.s * a.K + w0;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint16_t eps = a.eps[ci.s];
-  const float epsf = h2f(eps);
-  uint32_t T[kKG], need[kKG], off[kKG];
+  const _Float16 epsh = __builtin_bit_cast(_Float16, eps);
+  _Float16 vT[kKG];
+  uint32_t need[kKG], off[kKG];
   for (int g = 0; g < kKG; ++g) {
-    T[g] = g < nw ? a.sel[(sw0 + g) * 4 + 2] : 0xFFFFFFFFu;
+    vT[g] = __builtin_bit_cast(_Float16, g < nw ? okey_inv(a.sel[(sw0 + g) * 4 + 2]) : (uint16_t)0);
     need[g] = g < nw ? a.sel[(sw0 + g) * 4 + 3] : 0;
     off[g] = (g < nw && !(f & kSingle)) ? a.eqcnt[(int64_t)(w0 + g) * a.total_chunks + blockIdx.x] : 0;
     if (g < nw && a.rank_off) off[g] += a.rank_off[w0 + g];
   }
-  // phase A: every value's order key, and the rank of the values equal to T inside each wave
-  // (packed: key | rank in wave << 16 | equal << 23); one barrier for the whole block instead of two
-  // per (job slice, worker)
-  uint32_t pk[kJPT][kKG];
-  int32_t hbj[kJPT];
-  uint16_t cj[kJPT];
+  const bool retain = counter < 100;                 // retention bid of the previous winner
+  const bool leftover = counter > 1000 && w0 == 0;   // leftovers go to worker 0
+  uint32_t best[kJPT] = {};
+  uint64_t defer = 0;  // bit t * kKG + g: an equal value whose bid depends on its tie rank
+  ChunkScores cs;
+  load_chunk(a, ci, w0, cs);
   bool nob[kJPT];
-  const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
   for (int t = 0; t < kJPT; ++t) {
     const int64_t jj = t * 256 + threadIdx.x;
-    const bool live = jj < ci.nj;
-    const int64_t j = ci.j0 + jj;
-    hbj[t] = live ? a.hb[j] : -1;
-    cj[t] = live ? a.cost[j] : 0;
-    nob[t] = live && a.nobid[j];
-    uint16_t v[kKG];
+    nob[t] = leftover && jj < ci.nj && a.nobid[ci.j0 + jj];
+  }
 #pragma unroll
-    for (int g = 0; g < kKG; ++g) v[g] = (g < nw && live) ? wrow(a, ci, w0 + g)[j] : 0;
+  for (int t = 0; t < kJPT; ++t) {
+    const bool live = t * 256 + (int)threadIdx.x < ci.nj;
+    const int32_t hbj = live ? cs.hb[t] : -1;
 #pragma unroll
     for (int g = 0; g < kKG; ++g) {
-      uint32_t k = 0;
-      if (g < nw && live) k = okey(value_bits(w0 + g, v[g], hbj[t], cj[t]));
-      const bool eq = g < nw && live && k == T[g];
+      if (g >= nw) continue;
+      const int w = w0 + g;
+      const _Float16 x = value_h(w, cs.v[t][g], hbj, cs.c[t]);
+      const bool gt = live && x > vT[g];
+      const bool eq = live && x == vT[g];
       const unsigned long long m = __ballot(eq);
-      if (lane == 0) wcnt[t][g][wv] = __popcll(m);
-      pk[t][g] = k | ((uint32_t)__popcll(m & lt) << 16) | ((uint32_t)eq << 23) | ((uint32_t)live << 24);
+      if (lane == 0) eqm[t][g][wv] = m;
+      uint32_t bid = gt ? (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)((_Float16)(x - vT[g]) + epsh)) : 0u;
+      if ((retain && hbj == w) || (nob[t] && g == 0)) bid = eps;
+      else if (eq) defer |= 1ull << (t * kKG + g);
+      if (bid) best[t] = max(best[t], (bid << 16) | (0xFFFFu - (uint32_t)w));
     }
   }
   __syncthreads();
-  // phase B: bids in job order (the tie rank of a job = equal values at lower jobs of the segment)
-  uint32_t best[kJPT] = {};
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const uint64_t slice = 0x0001000100010001ull;  // bit t * kKG of every job slice t
 #pragma unroll
   for (int g = 0; g < kKG; ++g) {
-    const int w = w0 + g;
-    const float vT = h2f(okey_inv(T[g]));
+    if (g >= nw || !__ballot((defer & (slice << g)) != 0)) continue;
+    const uint32_t wbid = ((uint32_t)eps << 16) | (0xFFFFu - (uint32_t)(w0 + g));
     uint32_t run = off[g];
 #pragma unroll
     for (int t = 0; t < kJPT; ++t) {
-      const uint32_t c0 = wcnt[t][g][0], c1 = wcnt[t][g][1], c2 = wcnt[t][g][2], c3 = wcnt[t][g][3];
-      const uint32_t below = wv == 0 ? 0 : wv == 1 ? c0 : wv == 2 ? c0 + c1 : c0 + c1 + c2;
-      const uint32_t p = pk[t][g];
-      const uint32_t k = p & 0xFFFFu;
-      const bool eq = (p >> 23) & 1u, live = (p >> 24) & 1u;
-      const uint32_t before = run + below + ((p >> 16) & 63u);
-      run += c0 + c1 + c2 + c3;
-      uint16_t bid = 0;
-      if (live && k > T[g]) {
-        bid = f2h(h2f(f2h(h2f(okey_inv(k)) - vT)) + epsf);
-      } else if (eq && before < need[g]) {
-        bid = f2h(0.0f + epsf);
+      const unsigned long long m0 = eqm[t][g][0], m1 = eqm[t][g][1], m2 = eqm[t][g][2], m3 = eqm[t][g][3];
+      const uint32_t c0 = __popcll(m0), c1 = __popcll(m1), c2 = __popcll(m2);
+      if ((defer >> (t * kKG + g)) & 1ull) {
+        const unsigned long long mw = wv == 0 ? m0 : wv == 1 ? m1 : wv == 2 ? m2 : m3;
+        const uint32_t below = wv == 0 ? 0 : wv == 1 ? c0 : wv == 2 ? c0 + c1 : c0 + c1 + c2;
+        if (run + below + (uint32_t)__popcll(mw & lt) < need[g]) best[t] = max(best[t], wbid);
       }
-      if (counter < 100 && hbj[t] == w) bid = eps;        // retention bid of the previous winner
-      if (counter > 1000 && w == 0 && nob[t]) bid = eps;  // leftovers go to worker 0
-      if (bid && g < nw) best[t] = max(best[t], ((uint32_t)bid << 16) | (0xFFFFu - (uint32_t)w));
+      run += c0 + c1 + c2 + (uint32_t)__popcll(m3);
     }
   }
 #pragma unroll
@@ -511,8 +549,15 @@ __global__ __launch_bounds__(256) void sa_resolve_kernel(SegAuction a, int32_t* 
       a.nobid[j] = 1;
     }
   }
+  // one same-address atomic per block, not per wave: a segment's chunks all count into have[s]
+  __shared__ uint32_t wc[4];
   for (int o = 32; o > 0; o >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o);
-  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&a.have[ci.s], cnt);
+  if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t tot = wc[0] + wc[1] + wc[2] + wc[3];
+    if (tot) atomicAdd(&a.have[ci.s], tot);
+  }
 }
 
 // end of round r: a segment whose every job has a bidder is done after r+1 rounds
@@ -808,6 +853,8 @@ int rqsid_dauction_layout(int64_t n_local, int32_t n_workers, int64_t* offsets) 
   offsets[1] = (int64_t)((char*)a.hist - (char*)nullptr);   // u32 [K][256]
   offsets[2] = (int64_t)((char*)a.eqtot - (char*)nullptr);  // u32 [K]
   offsets[3] = (int64_t)((char*)a.have - (char*)nullptr);   // u32 [1]
+  offsets[4] = (int64_t)((char*)a.flag - (char*)nullptr);   // u8 [1]: bit 0 = still bidding
+  offsets[5] = 128;                                         // i32 [1]: rounds run (header, see dstate)
   return RQSID_OK;
 }
 

@@ -128,13 +128,15 @@ class GpuAuctionPasses:
         self.lib = lib
         self.wsb = int(lib.rqsid_dauction_workspace_bytes(self.n_local, self.k))
         self.ws = torch.zeros(self.wsb, dtype=torch.uint8, device=self.w.device)
-        offs = (ctypes.c_int64 * 4)()
+        offs = (ctypes.c_int64 * 6)()
         ops._lib.check(lib.rqsid_dauction_layout(self.n_local, self.k, offs), "rqsid_dauction_layout")
         k = self.k
         self._mm = self.ws[offs[0]:offs[0] + 8].view(torch.int32)
         self._hist = self.ws[offs[1]:offs[1] + k * 256 * 4].view(torch.int32).view(k, 256)
         self._eqtot = self.ws[offs[2]:offs[2] + k * 4].view(torch.int32)
         self._have = self.ws[offs[3]:offs[3] + 4].view(torch.int32)
+        self._flag = self.ws[offs[4]:offs[4] + 1]
+        self._rounds = self.ws[offs[5]:offs[5] + 4].view(torch.int32)
         self.out = torch.full((max(self.n_local, 1),), -1, dtype=torch.int32, device=self.w.device)
 
     def _args(self):
@@ -176,6 +178,13 @@ class GpuAuctionPasses:
     def end_round(self) -> None:
         ops._lib.check(self.lib.rqsid_dauction_end_round(*self._args(), *self._tail()), "rqsid_dauction_end_round")
 
+    def live(self) -> bool:
+        """Still bidding (host sync): end_round clears it once the reduced `have` covers every job."""
+        return bool(int(self._flag.item()) & 1)
+
+    def rounds_run(self) -> int:
+        return int(self._rounds.item())
+
     def result(self) -> torch.Tensor:
         return self.out[:self.n_local]
 
@@ -187,7 +196,11 @@ class ShardedAuction:
     to each worker's threshold are all-gathered (each rank's tie ranks start after the lower ranks'), and
     the count of jobs with a bidder is summed (all_reduce of one int32).  Every rank ends each round with
     identical thresholds and the same stop decision, and the assignment equals the single-process auction
-    of the whole matrix (same fp16 operations, same tie rule)."""
+    of the whole matrix (same fp16 operations, same tie rule).  The stop decision is taken on the device
+    (end_round clears the live flag; later passes are no-ops), so the host reads it once per ``poll``
+    rounds instead of synchronising every round."""
+
+    poll = 8
 
     def __init__(self, group=None):
         self.group = group
@@ -223,7 +236,7 @@ class ShardedAuction:
         self._all_reduce(mx, dist.ReduceOp.MAX)
         self._all_reduce(mn, dist.ReduceOp.MIN)
         passes.set_minmax(int(mx.item()), int(mn.item()))
-        rounds = 0
+        issued = 0
         while True:
             for low in (0, 1):
                 h = passes.hist(low)
@@ -237,12 +250,13 @@ class ShardedAuction:
             passes.bid(rank_off)
             have = passes.resolve()
             self._all_reduce(have)
-            done = int(have.item()) == n_global  # read before end_round clears the counter
-            passes.end_round()
-            rounds += 1
-            if done:
-                return passes.result(), rounds
-            if max_rounds and rounds >= max_rounds:
+            passes.end_round()  # the device compares the reduced count with n_global
+            issued += 1
+            if issued % self.poll and not (max_rounds and issued >= max_rounds):
+                continue
+            if not passes.live():
+                return passes.result(), passes.rounds_run()
+            if max_rounds and issued >= max_rounds:
                 raise RuntimeError(f"auction: no complete assignment after {max_rounds} rounds")
 
 
