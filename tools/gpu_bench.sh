@@ -10,3 +10,6 @@ timeout -k 10 600 python bench.py --traffic-json "$OUT/traffic/traffic.json" > "
 cat "$OUT/bench.json"
 (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu --traffic-json "$OUT/traffic/traffic.json" > "$OUT/prof_bench.json" 2> "$OUT/prof.err") || { tail -20 "$OUT/prof.err"; exit 1; }
 python tools/prof_summary.py "$OUT/prof/run_results.db" > "$OUT/kernels.txt" && head -12 "$OUT/kernels.txt"
+# keep gpurun_out small (the merge back is capped at 64 MiB): drop the raw databases once summarised
+rm -rf "$OUT/prof/"*.db "$OUT/prof/"*/ "$OUT/traffic/p1" "$OUT/traffic/p2" 2>/dev/null
+du -sh "$OUT"
