@@ -26,6 +26,7 @@ namespace {
 constexpr int kKG = 16;        // workers per block
 constexpr int kCh = 1024;      // jobs per chunk
 constexpr int kJPT = kCh / 256;
+constexpr int kAbovePad = 32;  // u32 per worker in SegAuction::above
 static_assert(kJPT * kKG == 64, "sa_bid_kernel keeps one deferral bit per (job slice, worker) in a u64");
 
 __device__ __forceinline__ float h2f(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
@@ -71,6 +72,13 @@ struct SegAuction {
   int64_t n_glob;                // 0: single process
   const uint32_t* rank_off;      // [K] or null
   uint32_t* eqtot;               // [S*K] equal-to-T values per (segment, worker) on this rank
+  // guessed high byte (single-process multi-chunk segments; null in the row-sharded mode): one sweep
+  // histograms the low bytes of the values in last round's bin b1 and counts the values above it; when
+  // the threshold is still in b1 that is the exact selection, otherwise (miss) the worker takes the
+  // two-pass selection this round
+  uint32_t* above;               // [n_multi*K][kAbovePad] values with high byte > b1 (one line per worker:
+                                 // every chunk block adds to it)
+  uint8_t* miss;                 // [n_multi*K]
 };
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ off, int n_seg, int64_t i) {
@@ -252,23 +260,33 @@ __device__ __forceinline__ void wave_select(const uint32_t* __restrict__ h, uint
   above = (uint32_t)__shfl((int)ab, L);
 }
 
-// multi-chunk segments: global histograms
-template <bool LOW>
+// multi-chunk segments: global histograms.  MODE 0: high bytes, 1: low bytes of the values in the
+// selected bin b1 (sel[0]), 2: low bytes of the values in last round's bin b1 (sel[0]) plus the count of
+// values above it (the guessed pass).  With the guessed pass on (a.miss), modes 0 and 1 run only for the
+// workers it missed.
+template <int MODE>
 __global__ __launch_bounds__(256) void sa_hist_kernel(SegAuction a) {
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
   if (!(f & kLive) || (f & kSingle)) return;
   __shared__ uint32_t h[kKG][256];
+  __shared__ uint32_t abv[kKG];
   const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
   const int lane = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < kKG * 256; i += 256) (&h[0][0])[i] = 0;
-  __syncthreads();
   const int64_t sw0 = (int64_t)ci.s * a.K + w0;
   const int64_t hw0 = (int64_t)a.hidx[ci.s] * a.K + w0;
+  uint32_t part = (1u << nw) - 1u;  // workers taking this pass
+  if (MODE != 2 && a.miss) {
+    part = 0;
+    for (int g = 0; g < nw; ++g) part |= (uint32_t)(a.miss[hw0 + g] != 0) << g;
+    if (!part) return;
+  }
+  for (int i = threadIdx.x; i < kKG * 256; i += 256) (&h[0][0])[i] = 0;
+  if (threadIdx.x < kKG) abv[threadIdx.x] = 0;
+  __syncthreads();
   // high-byte pass: a worker's values crowd into one or two high-byte bins, where same-address LDS
   // atomics serialise a wave 64-fold.  The bins at and just below last round's threshold (sel[0]; any
   // value is correct, it only decides which bins take the fast path) are counted with ballots.
-  // low-byte pass: only the values in the selected bin b1 count.
   uint32_t b1[kKG], n0[kKG] = {}, n1[kKG] = {};
   for (int g = 0; g < kKG; ++g) b1[g] = g < nw ? a.sel[(sw0 + g) * 4 + 0] & 255u : 0;
   ChunkScores cs;
@@ -278,10 +296,11 @@ __global__ __launch_bounds__(256) void sa_hist_kernel(SegAuction a) {
     const bool live = t * 256 + (int)threadIdx.x < ci.nj;
 #pragma unroll
     for (int g = 0; g < kKG; ++g) {
-      if (g >= nw) continue;
+      if (!((part >> g) & 1u)) continue;
       const uint32_t k = okey(value_bits(w0 + g, cs.v[t][g], cs.hb[t], cs.c[t]));
-      if (LOW) {
+      if (MODE != 0) {
         if (live && (k >> 8) == b1[g]) atomicAdd(&h[g][k & 255], 1u);
+        if (MODE == 2) n0[g] += (uint32_t)__popcll(__ballot(live && (k >> 8) > b1[g]));
       } else {
         const uint32_t d = b1[g] - (k >> 8);  // 0: the guessed bin, 1: the bin below
         n0[g] += (uint32_t)__popcll(__ballot(live && d == 0));
@@ -290,15 +309,20 @@ __global__ __launch_bounds__(256) void sa_hist_kernel(SegAuction a) {
       }
     }
   }
-  if (!LOW && lane == 0) {
+  if (MODE == 0 && lane == 0) {
     for (int g = 0; g < nw; ++g) {
       if (n0[g]) atomicAdd(&h[g][b1[g]], n0[g]);
       if (n1[g]) atomicAdd(&h[g][b1[g] - 1], n1[g]);  // n1 > 0 implies b1 >= 1
     }
   }
+  if (MODE == 2 && lane == 0) {
+    for (int g = 0; g < nw; ++g)
+      if (n0[g]) atomicAdd(&abv[g], n0[g]);
+  }
   __syncthreads();
+  if (MODE == 2 && threadIdx.x < nw && abv[threadIdx.x]) atomicAdd(&a.above[(hw0 + threadIdx.x) * kAbovePad], abv[threadIdx.x]);
   for (int i = threadIdx.x; i < nw * 256; i += 256) {
-    const uint32_t c = (&h[0][0])[i];
+    const uint32_t c = (&h[0][0])[i];  // zero for the workers that did not take part
     if (c) atomicAdd(&a.hist[(hw0 + i / 256) * 256 + (i & 255)], c);
   }
 }
@@ -311,6 +335,7 @@ __global__ __launch_bounds__(256) void sa_select_kernel(SegAuction a) {
   const int s = a.mseg[hw / a.K];
   const int w = (int)(hw % a.K);
   if (!(a.flag[s] & kLive)) return;
+  if (a.miss && !a.miss[hw]) return;  // the guessed pass found this worker's threshold
   const int64_t n_s = a.n_glob ? a.n_glob : a.seg_off[s + 1] - a.seg_off[s];
   const uint32_t jpw = (uint32_t)(n_s / a.K);
   uint32_t* h = a.hist + hw * 256;
@@ -332,6 +357,37 @@ __global__ __launch_bounds__(256) void sa_select_kernel(SegAuction a) {
     }
   }
   for (int i = lane; i < 256; i += 64) h[i] = 0;  // ready for the next histogram
+}
+
+// the guessed pass's selection: exact when the (jpw+1)-th largest value lies in last round's bin b1
+// (values above b1 < rank <= values at or above b1); otherwise a miss for the two-pass selection
+__global__ __launch_bounds__(256) void sa_select_guess_kernel(SegAuction a) {
+  const int64_t hw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (hw >= (int64_t)a.n_multi * a.K) return;
+  const int s = a.mseg[hw / a.K];
+  const int w = (int)(hw % a.K);
+  if (!(a.flag[s] & kLive)) return;
+  const int lane = threadIdx.x & 63;
+  const uint32_t jpw = (uint32_t)((a.seg_off[s + 1] - a.seg_off[s]) / a.K);
+  const uint32_t rank = jpw + 1;
+  uint32_t* h = a.hist + hw * 256;
+  uint32_t* sel = a.sel + ((int64_t)s * a.K + w) * 4;
+  const uint32_t ab = a.above[hw * kAbovePad];
+  uint32_t cnt = h[lane] + h[lane + 64] + h[lane + 128] + h[lane + 192];
+  for (int o = 32; o > 0; o >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o);
+  const bool hit = ab < rank && rank <= ab + cnt;
+  uint32_t b = 0, above = 0;
+  if (hit) wave_select(h, rank - ab, b, above);
+  if (lane == 0) {
+    if (hit) {
+      sel[0] &= 255u;
+      sel[2] = (sel[0] << 8) | b;
+      sel[3] = jpw - (ab + above);
+    }
+    a.miss[hw] = hit ? 0 : 1;
+    a.above[hw * kAbovePad] = 0;
+  }
+  for (int i = lane; i < 256; i += 64) h[i] = 0;
 }
 
 // one-chunk segments: both histogram passes and both selections inside the block; the chunk offset of
@@ -622,7 +678,7 @@ struct Carve {
 };
 
 // workspace layout (also the size query when p == nullptr)
-void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t total_chunks) {
+void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t total_chunks, bool guess) {
   a.flag = c.take<uint8_t>(S);
   a.eps = c.take<uint16_t>(S);
   a.mm = c.take<uint32_t>(2 * (int64_t)S);
@@ -639,6 +695,8 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.sel = c.take<uint32_t>((int64_t)S * K * 4);
   a.eqcnt = c.take<uint32_t>((int64_t)K * total_chunks);
   a.eqtot = c.take<uint32_t>((int64_t)S * K);
+  a.above = guess ? c.take<uint32_t>((int64_t)a.n_multi * K * kAbovePad) : nullptr;
+  a.miss = guess ? c.take<uint8_t>((int64_t)a.n_multi * K) : nullptr;
 }
 
 }  // namespace
@@ -656,7 +714,7 @@ int64_t rqsid_seg_auction_workspace_bytes(int64_t n_jobs, int32_t n_workers, int
   SegAuction a{};
   a.n_multi = n_multi;
   Carve c{nullptr};
-  carve(a, c, n_jobs, n_workers, n_seg, total_chunks);
+  carve(a, c, n_jobs, n_workers, n_seg, total_chunks, true);
   return c.used;
 }
 
@@ -684,7 +742,7 @@ int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_
   a.rounds = out_rounds;
   a.n_multi = n_multi;
   Carve c{(char*)workspace};
-  carve(a, c, n_jobs, n_workers, n_seg, total_chunks);
+  carve(a, c, n_jobs, n_workers, n_seg, total_chunks, true);
   const unsigned gs = (unsigned)cdiv(n_seg, 256);
   uint32_t* host = nullptr;  // pinned readback: [0] live segments, [1] multi-chunk segments
   if (hipHostMalloc((void**)&host, 2 * sizeof(uint32_t)) != hipSuccess)
@@ -707,7 +765,10 @@ int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_
     return RQSID_OK;
   }
   const bool any_single = n_multi < n_seg;
-  if (n_multi > 0 && hipMemsetAsync(a.hist, 0, (size_t)n_multi * n_workers * 256 * 4, st) != hipSuccess) {
+  const size_t mk = (size_t)n_multi * n_workers;
+  if (n_multi > 0 && (hipMemsetAsync(a.hist, 0, mk * 256 * 4, st) != hipSuccess ||
+                      hipMemsetAsync(a.above, 0, mk * kAbovePad * 4, st) != hipSuccess ||
+                      hipMemsetAsync(a.miss, 1, mk, st) != hipSuccess)) {
     (void)hipHostFree(host);
     return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   }
@@ -729,9 +790,13 @@ int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_
   constexpr int kPoll = 8;
   auto launch_round = [&](hipStream_t q, bool count) {
     if (n_multi > 0) {
-      hipLaunchKernelGGL((sa_hist_kernel<false>), gcw, dim3(256), 0, q, a);
+      hipLaunchKernelGGL((sa_hist_kernel<2>), gcw, dim3(256), 0, q, a);
+      hipLaunchKernelGGL(sa_select_guess_kernel, dim3(gmw), dim3(256), 0, q, a);
+      // the two-pass selection for the workers the guessed pass missed (every block exits at once
+      // when none of its workers missed)
+      hipLaunchKernelGGL((sa_hist_kernel<0>), gcw, dim3(256), 0, q, a);
       hipLaunchKernelGGL((sa_select_kernel<false>), dim3(gmw), dim3(256), 0, q, a);
-      hipLaunchKernelGGL((sa_hist_kernel<true>), gcw, dim3(256), 0, q, a);
+      hipLaunchKernelGGL((sa_hist_kernel<1>), gcw, dim3(256), 0, q, a);
       hipLaunchKernelGGL((sa_select_kernel<true>), dim3(gmw), dim3(256), 0, q, a);
       hipLaunchKernelGGL(sa_eqcount_kernel, gcw, dim3(256), 0, q, a);
       hipLaunchKernelGGL(sa_eqscan_kernel, dim3(gmw), dim3(256), 0, q, a);
@@ -822,7 +887,7 @@ int dstate(SegAuction& a, const uint16_t* scores, int32_t k, int64_t n_local, in
   a.chunk_off = (const int32_t*)(p + 64);
   a.rounds = (int32_t*)(p + 128);
   Carve c{p + kDHeader};
-  carve(a, c, n_local, k, 1, nch);
+  carve(a, c, n_local, k, 1, nch, false);
   if (wsb < kDHeader + c.used) return fail(RQSID_E_WORKSPACE, "dauction: workspace too small");
   return RQSID_OK;
 }
@@ -831,7 +896,7 @@ int64_t dws(int64_t n_local, int32_t k) {
   SegAuction a{};
   a.n_multi = 1;
   Carve c{nullptr};
-  carve(a, c, n_local, k, 1, cdiv(n_local, kCh));
+  carve(a, c, n_local, k, 1, cdiv(n_local, kCh), false);
   return kDHeader + c.used;
 }
 }  // namespace
@@ -848,7 +913,7 @@ int rqsid_dauction_layout(int64_t n_local, int32_t n_workers, int64_t* offsets) 
   SegAuction a{};
   a.n_multi = 1;
   Carve c{(char*)nullptr + kDHeader};
-  carve(a, c, n_local, n_workers, 1, cdiv(n_local, kCh));
+  carve(a, c, n_local, n_workers, 1, cdiv(n_local, kCh), false);
   offsets[0] = (int64_t)((char*)a.mm - (char*)nullptr);     // u32 [2]: max key, min key
   offsets[1] = (int64_t)((char*)a.hist - (char*)nullptr);   // u32 [K][256]
   offsets[2] = (int64_t)((char*)a.eqtot - (char*)nullptr);  // u32 [K]
@@ -897,8 +962,8 @@ int rqsid_dauction_hist(const uint16_t* scores, int32_t n_workers, int64_t n_loc
   if (rc) return rc;
   if (n_local == 0) return RQSID_OK;
   const dim3 g((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG));
-  if (low) hipLaunchKernelGGL((sa_hist_kernel<true>), g, dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL((sa_hist_kernel<false>), g, dim3(256), 0, (hipStream_t)stream, a);
+  if (low) hipLaunchKernelGGL((sa_hist_kernel<1>), g, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL((sa_hist_kernel<0>), g, dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("dauction_hist");
 }
 
