@@ -27,7 +27,8 @@ constexpr int kKG = 16;        // workers per block
 constexpr int kCh = 1024;      // jobs per chunk
 constexpr int kJPT = kCh / 256;
 constexpr int kAbovePad = 32;  // u32 per worker in SegAuction::above
-static_assert(kJPT * kKG == 64, "sa_bid_kernel keeps one deferral bit per (job slice, worker) in a u64");
+static_assert(kJPT * kKG == 64, "sa_bid_kernel keeps one deferral bit per (job slice, worker) in a u64, "
+              "and its 64 x 4 eqm slots are zeroed by the 256 threads");
 
 __device__ __forceinline__ float h2f(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
 __device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
@@ -532,6 +533,8 @@ __global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a) {
   uint64_t defer = 0;  // bit t * kKG + g: an equal value whose bid depends on its tie rank
   ChunkScores cs;
   load_chunk(a, ci, w0, cs);
+  (&eqm[0][0][0])[threadIdx.x] = 0;  // kJPT * kKG * 4 == 256 slots
+  __syncthreads();
   bool nob[kJPT];
 #pragma unroll
   for (int t = 0; t < kJPT; ++t) {
@@ -547,10 +550,13 @@ __global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a) {
       if (g >= nw) continue;
       const int w = w0 + g;
       const _Float16 x = value_h(w, cs.v[t][g], hbj, cs.c[t]);
+      // about 1/K of the values reach T: a wave whose lanes are all below it and under no override
+      // has nothing to bid or to count (its eqm slot stays zero)
+      if (!__ballot(live && (x >= vT[g] || (retain && hbj == w) || (g == 0 && nob[t])))) continue;
       const bool gt = live && x > vT[g];
       const bool eq = live && x == vT[g];
       const unsigned long long m = __ballot(eq);
-      if (lane == 0) eqm[t][g][wv] = m;
+      if (lane == 0 && m) eqm[t][g][wv] = m;
       uint32_t bid = gt ? (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)((_Float16)(x - vT[g]) + epsh)) : 0u;
       if ((retain && hbj == w) || (nob[t] && g == 0)) bid = eps;
       else if (eq) defer |= 1ull << (t * kKG + g);
