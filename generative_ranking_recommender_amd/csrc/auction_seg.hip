@@ -27,7 +27,7 @@ constexpr int kKG = 16;        // workers per block
 constexpr int kCh = 1024;      // jobs per chunk
 constexpr int kJPT = kCh / 256;
 constexpr int kAbovePad = 32;  // u32 per worker in SegAuction::above
-static_assert(kJPT * kKG == 64, "sa_bid_kernel keeps one deferral bit per (job slice, worker) in a u64, "
+static_assert(kJPT == 4 && kJPT * kKG == 64, "load_chunk<true> takes 4 jobs per lane; sa_bid_kernel keeps one deferral bit per (job slice, worker) in a u64, "
               "and its 64 x 4 eqm slots are zeroed by the 256 threads");
 
 __device__ __forceinline__ float h2f(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
@@ -138,7 +138,38 @@ struct ChunkScores {
   uint16_t c[kJPT];
 };
 
+// Job of slice t for this thread: slice-major (t * 256 + thread) in general; with VEC every lane takes
+// four consecutive jobs (4 * thread + t) and loads them with one 8-byte load per worker row, which needs
+// 8-byte aligned rows and chunks of a multiple of 4 jobs (the single auction with N % 4 == 0).
+template <bool VEC>
+__device__ __forceinline__ int64_t job_of(int t) {
+  return VEC ? 4 * (int64_t)threadIdx.x + t : (int64_t)t * 256 + threadIdx.x;
+}
+
+template <bool VEC>
 __device__ __forceinline__ void load_chunk(const SegAuction& a, const ChunkInfo& ci, int w0, ChunkScores& cs) {
+  if (VEC) {
+    const int64_t j = ci.j0 + min(4 * (int64_t)threadIdx.x, ci.nj - 4);
+    const int4 hb4 = *reinterpret_cast<const int4*>(a.hb + j);
+    const uint2 c4 = *reinterpret_cast<const uint2*>(a.cost + j);
+    cs.hb[0] = hb4.x;
+    cs.hb[1] = hb4.y;
+    cs.hb[2] = hb4.z;
+    cs.hb[3] = hb4.w;
+    cs.c[0] = (uint16_t)c4.x;
+    cs.c[1] = (uint16_t)(c4.x >> 16);
+    cs.c[2] = (uint16_t)c4.y;
+    cs.c[3] = (uint16_t)(c4.y >> 16);
+#pragma unroll
+    for (int g = 0; g < kKG; ++g) {
+      const uint2 q = *reinterpret_cast<const uint2*>(wrow(a, ci, min(w0 + g, a.K - 1)) + j);
+      cs.v[0][g] = (uint16_t)q.x;
+      cs.v[1][g] = (uint16_t)(q.x >> 16);
+      cs.v[2][g] = (uint16_t)q.y;
+      cs.v[3][g] = (uint16_t)(q.y >> 16);
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < kJPT; ++t) {
     const int64_t j = ci.j0 + min((int64_t)(t * 256 + threadIdx.x), ci.nj - 1);
@@ -265,7 +296,7 @@ __device__ __forceinline__ void wave_select(const uint32_t* __restrict__ h, uint
 // selected bin b1 (sel[0]), 2: low bytes of the values in last round's bin b1 (sel[0]) plus the count of
 // values above it (the guessed pass).  With the guessed pass on (a.miss), modes 0 and 1 run only for the
 // workers it missed.
-template <int MODE>
+template <int MODE, bool VEC>
 __global__ __launch_bounds__(256) void sa_hist_kernel(SegAuction a) {
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
@@ -291,10 +322,10 @@ __global__ __launch_bounds__(256) void sa_hist_kernel(SegAuction a) {
   uint32_t b1[kKG], n0[kKG] = {}, n1[kKG] = {};
   for (int g = 0; g < kKG; ++g) b1[g] = g < nw ? a.sel[(sw0 + g) * 4 + 0] & 255u : 0;
   ChunkScores cs;
-  load_chunk(a, ci, w0, cs);
+  load_chunk<VEC>(a, ci, w0, cs);
 #pragma unroll
   for (int t = 0; t < kJPT; ++t) {
-    const bool live = t * 256 + (int)threadIdx.x < ci.nj;
+    const bool live = job_of<VEC>(t) < ci.nj;
 #pragma unroll
     for (int g = 0; g < kKG; ++g) {
       if (!((part >> g) & 1u)) continue;
@@ -447,6 +478,7 @@ __global__ __launch_bounds__(256) void sa_small_select_kernel(SegAuction a) {
 }
 
 // ---- tie counts (multi-chunk segments) ----
+template <bool VEC>
 __global__ __launch_bounds__(256) void sa_eqcount_kernel(SegAuction a) {
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
@@ -461,10 +493,10 @@ __global__ __launch_bounds__(256) void sa_eqcount_kernel(SegAuction a) {
     vT[g] = __builtin_bit_cast(_Float16, g < nw ? okey_inv(a.sel[(sw0 + g) * 4 + 2]) : (uint16_t)0);
   uint32_t cnt[kKG] = {};
   ChunkScores cs;
-  load_chunk(a, ci, w0, cs);
+  load_chunk<VEC>(a, ci, w0, cs);
 #pragma unroll
   for (int t = 0; t < kJPT; ++t) {
-    const bool live = t * 256 + (int)threadIdx.x < ci.nj;
+    const bool live = job_of<VEC>(t) < ci.nj;
 #pragma unroll
     for (int g = 0; g < kKG; ++g)
       if (g < nw) cnt[g] += live && value_h(w0 + g, cs.v[t][g], cs.hb[t], cs.c[t]) == vT[g];
@@ -508,6 +540,7 @@ __global__ __launch_bounds__(256) void sa_eqscan_kernel(SegAuction a) {
 // leftover overrides) in one pass in fp16 and records each wave's ballot of the values equal to T.
 // Phase B visits only the (job slice, worker) pairs where some lane holds an equal value whose bid
 // depends on its rank among the segment's equal values in job order.
+template <bool VEC>
 __global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a) {
   const int counter = *a.round_dev;
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
@@ -532,18 +565,19 @@ __global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a) {
   uint32_t best[kJPT] = {};
   uint64_t defer = 0;  // bit t * kKG + g: an equal value whose bid depends on its tie rank
   ChunkScores cs;
-  load_chunk(a, ci, w0, cs);
+  load_chunk<VEC>(a, ci, w0, cs);
   (&eqm[0][0][0])[threadIdx.x] = 0;  // kJPT * kKG * 4 == 256 slots
   __syncthreads();
   bool nob[kJPT];
 #pragma unroll
   for (int t = 0; t < kJPT; ++t) {
     const int64_t jj = t * 256 + threadIdx.x;
-    nob[t] = leftover && jj < ci.nj && a.nobid[ci.j0 + jj];
+    (void)jj;
+    nob[t] = leftover && job_of<VEC>(t) < ci.nj && a.nobid[ci.j0 + job_of<VEC>(t)];
   }
 #pragma unroll
   for (int t = 0; t < kJPT; ++t) {
-    const bool live = t * 256 + (int)threadIdx.x < ci.nj;
+    const bool live = job_of<VEC>(t) < ci.nj;
     const int32_t hbj = live ? cs.hb[t] : -1;
 #pragma unroll
     for (int g = 0; g < kKG; ++g) {
@@ -570,6 +604,24 @@ __global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a) {
   for (int g = 0; g < kKG; ++g) {
     if (g >= nw || !__ballot((defer & (slice << g)) != 0)) continue;
     const uint32_t wbid = ((uint32_t)eps << 16) | (0xFFFFu - (uint32_t)(w0 + g));
+    if (VEC) {
+      // job order: earlier waves, then lower lanes (all four slices), then this lane's earlier slices
+      uint32_t before = off[g], own = 0;
+#pragma unroll
+      for (int t = 0; t < kJPT; ++t) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const unsigned long long m = eqm[t][g][q];
+          before += q < wv ? (uint32_t)__popcll(m) : q == wv ? (uint32_t)__popcll(m & lt) : 0u;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < kJPT; ++t) {
+        if (((defer >> (t * kKG + g)) & 1ull) && before + own < need[g]) best[t] = max(best[t], wbid);
+        own += (uint32_t)((eqm[t][g][wv] >> lane) & 1ull);
+      }
+      continue;
+    }
     uint32_t run = off[g];
 #pragma unroll
     for (int t = 0; t < kJPT; ++t) {
@@ -585,7 +637,7 @@ __global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a) {
   }
 #pragma unroll
   for (int t = 0; t < kJPT; ++t)
-    if (best[t]) atomicMax(&a.key[ci.j0 + t * 256 + threadIdx.x], best[t]);
+    if (best[t]) atomicMax(&a.key[ci.j0 + job_of<VEC>(t)], best[t]);
 }
 
 // ---- resolve: per job of the live segments, one block per chunk ----
@@ -728,6 +780,19 @@ int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_
                                const int32_t* seg_chunk_off, int64_t total_chunks, int32_t n_multi, int64_t n_jobs,
                                const uint8_t* active, int32_t max_rounds, int32_t* out_assign, int32_t* out_rounds,
                                void* workspace, int64_t workspace_bytes, void* stream) {
+  return rqsid::seg_auction_run(scores, n_workers, n_seg, seg_off, seg_chunk_off, total_chunks, n_multi, n_jobs,
+                                active, max_rounds, out_assign, out_rounds, workspace, workspace_bytes, stream, false);
+}
+
+}  // extern "C"
+
+namespace rqsid {
+// vec: one segment whose rows and chunks allow 8-byte loads (rqsid_auction_lap_half with N % 4 == 0)
+int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, const int32_t* seg_off,
+                    const int32_t* seg_chunk_off, int64_t total_chunks, int32_t n_multi, int64_t n_jobs,
+                    const uint8_t* active, int32_t max_rounds, int32_t* out_assign, int32_t* out_rounds,
+                    void* workspace, int64_t workspace_bytes, void* stream, bool vec) {
+  vec = vec && n_seg == 1 && n_jobs % 4 == 0 && ((uintptr_t)scores & 7) == 0;
   if (!scores || !seg_off || !seg_chunk_off || !out_assign || !out_rounds || n_workers <= 0 || n_seg <= 0 ||
       total_chunks < 0 || total_chunks > INT32_MAX || n_jobs < 0 || n_jobs > INT32_MAX || n_multi < 0 ||
       n_multi > n_seg)
@@ -796,19 +861,24 @@ int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_
   constexpr int kPoll = 8;
   auto launch_round = [&](hipStream_t q, bool count) {
     if (n_multi > 0) {
-      hipLaunchKernelGGL((sa_hist_kernel<2>), gcw, dim3(256), 0, q, a);
+      if (vec) hipLaunchKernelGGL((sa_hist_kernel<2, true>), gcw, dim3(256), 0, q, a);
+      else hipLaunchKernelGGL((sa_hist_kernel<2, false>), gcw, dim3(256), 0, q, a);
       hipLaunchKernelGGL(sa_select_guess_kernel, dim3(gmw), dim3(256), 0, q, a);
       // the two-pass selection for the workers the guessed pass missed (every block exits at once
       // when none of its workers missed)
-      hipLaunchKernelGGL((sa_hist_kernel<0>), gcw, dim3(256), 0, q, a);
+      if (vec) hipLaunchKernelGGL((sa_hist_kernel<0, true>), gcw, dim3(256), 0, q, a);
+      else hipLaunchKernelGGL((sa_hist_kernel<0, false>), gcw, dim3(256), 0, q, a);
       hipLaunchKernelGGL((sa_select_kernel<false>), dim3(gmw), dim3(256), 0, q, a);
-      hipLaunchKernelGGL((sa_hist_kernel<1>), gcw, dim3(256), 0, q, a);
+      if (vec) hipLaunchKernelGGL((sa_hist_kernel<1, true>), gcw, dim3(256), 0, q, a);
+      else hipLaunchKernelGGL((sa_hist_kernel<1, false>), gcw, dim3(256), 0, q, a);
       hipLaunchKernelGGL((sa_select_kernel<true>), dim3(gmw), dim3(256), 0, q, a);
-      hipLaunchKernelGGL(sa_eqcount_kernel, gcw, dim3(256), 0, q, a);
+      if (vec) hipLaunchKernelGGL((sa_eqcount_kernel<true>), gcw, dim3(256), 0, q, a);
+      else hipLaunchKernelGGL((sa_eqcount_kernel<false>), gcw, dim3(256), 0, q, a);
       hipLaunchKernelGGL(sa_eqscan_kernel, dim3(gmw), dim3(256), 0, q, a);
     }
     if (any_single) hipLaunchKernelGGL(sa_small_select_kernel, gcw, dim3(256), 0, q, a);
-    hipLaunchKernelGGL(sa_bid_kernel, gcw, dim3(256), 0, q, a);
+    if (vec) hipLaunchKernelGGL((sa_bid_kernel<true>), gcw, dim3(256), 0, q, a);
+    else hipLaunchKernelGGL((sa_bid_kernel<false>), gcw, dim3(256), 0, q, a);
     hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, q, a, out_assign);
     hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
     hipLaunchKernelGGL(sa_round_inc_kernel, dim3(1), dim3(1), 0, q, a);
@@ -857,7 +927,7 @@ int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_
   return rc;
 }
 
-}  // extern "C"
+}  // namespace rqsid
 
 // ---------------------------------------------------------------------------------------------------------
 // Row-sharded single auction, one pass per call (distributed.ShardedAuction drives the rounds and the
@@ -968,8 +1038,8 @@ int rqsid_dauction_hist(const uint16_t* scores, int32_t n_workers, int64_t n_loc
   if (rc) return rc;
   if (n_local == 0) return RQSID_OK;
   const dim3 g((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG));
-  if (low) hipLaunchKernelGGL((sa_hist_kernel<1>), g, dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL((sa_hist_kernel<0>), g, dim3(256), 0, (hipStream_t)stream, a);
+  if (low) hipLaunchKernelGGL((sa_hist_kernel<1, false>), g, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL((sa_hist_kernel<0, false>), g, dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("dauction_hist");
 }
 
@@ -997,7 +1067,7 @@ int rqsid_dauction_eqcount(const uint16_t* scores, int32_t n_workers, int64_t n_
       return fail(RQSID_E_LAUNCH, "dauction: memset");
     return RQSID_OK;
   }
-  hipLaunchKernelGGL(sa_eqcount_kernel, dim3((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG)), dim3(256), 0,
+  hipLaunchKernelGGL((sa_eqcount_kernel<false>), dim3((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG)), dim3(256), 0,
                      st, a);
   hipLaunchKernelGGL(sa_eqscan_kernel, dim3((unsigned)cdiv(n_workers, 4)), dim3(256), 0, st, a);
   return check_launch("dauction_eqcount");
@@ -1011,7 +1081,7 @@ int rqsid_dauction_bid(const uint16_t* scores, int32_t n_workers, int64_t n_loca
   if (rc) return rc;
   if (n_local == 0) return RQSID_OK;
   a.rank_off = rank_off;
-  hipLaunchKernelGGL(sa_bid_kernel, dim3((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG)), dim3(256), 0,
+  hipLaunchKernelGGL((sa_bid_kernel<false>), dim3((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG)), dim3(256), 0,
                      (hipStream_t)stream, a);
   return check_launch("dauction_bid");
 }
