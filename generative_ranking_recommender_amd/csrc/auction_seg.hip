@@ -968,6 +968,11 @@ int dstate(SegAuction& a, const uint16_t* scores, int32_t k, int64_t n_local, in
   return RQSID_OK;
 }
 
+// a rank's share takes the 8-byte-load sweeps when its rows and chunks allow them (load_chunk<true>)
+bool dvec(const uint16_t* scores, int64_t n_local) {
+  return n_local % 4 == 0 && ((uintptr_t)scores & 7) == 0;
+}
+
 int64_t dws(int64_t n_local, int32_t k) {
   SegAuction a{};
   a.n_multi = 1;
@@ -1038,8 +1043,12 @@ int rqsid_dauction_hist(const uint16_t* scores, int32_t n_workers, int64_t n_loc
   if (rc) return rc;
   if (n_local == 0) return RQSID_OK;
   const dim3 g((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG));
-  if (low) hipLaunchKernelGGL((sa_hist_kernel<1, false>), g, dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL((sa_hist_kernel<0, false>), g, dim3(256), 0, (hipStream_t)stream, a);
+  hipStream_t st = (hipStream_t)stream;
+  const bool vec = dvec(scores, n_local);
+  if (low && vec) hipLaunchKernelGGL((sa_hist_kernel<1, true>), g, dim3(256), 0, st, a);
+  else if (low) hipLaunchKernelGGL((sa_hist_kernel<1, false>), g, dim3(256), 0, st, a);
+  else if (vec) hipLaunchKernelGGL((sa_hist_kernel<0, true>), g, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((sa_hist_kernel<0, false>), g, dim3(256), 0, st, a);
   return check_launch("dauction_hist");
 }
 
@@ -1067,8 +1076,9 @@ int rqsid_dauction_eqcount(const uint16_t* scores, int32_t n_workers, int64_t n_
       return fail(RQSID_E_LAUNCH, "dauction: memset");
     return RQSID_OK;
   }
-  hipLaunchKernelGGL((sa_eqcount_kernel<false>), dim3((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG)), dim3(256), 0,
-                     st, a);
+  const dim3 g((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG));
+  if (dvec(scores, n_local)) hipLaunchKernelGGL((sa_eqcount_kernel<true>), g, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((sa_eqcount_kernel<false>), g, dim3(256), 0, st, a);
   hipLaunchKernelGGL(sa_eqscan_kernel, dim3((unsigned)cdiv(n_workers, 4)), dim3(256), 0, st, a);
   return check_launch("dauction_eqcount");
 }
@@ -1081,8 +1091,9 @@ int rqsid_dauction_bid(const uint16_t* scores, int32_t n_workers, int64_t n_loca
   if (rc) return rc;
   if (n_local == 0) return RQSID_OK;
   a.rank_off = rank_off;
-  hipLaunchKernelGGL((sa_bid_kernel<false>), dim3((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG)), dim3(256), 0,
-                     (hipStream_t)stream, a);
+  const dim3 g((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG));
+  if (dvec(scores, n_local)) hipLaunchKernelGGL((sa_bid_kernel<true>), g, dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL((sa_bid_kernel<false>), g, dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("dauction_bid");
 }
 

@@ -242,7 +242,8 @@ def _gpu_sharded_auction_worker(rank, world, port, w16, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,k,levels", [(3000, 16, 7), (640, 64, 1000)])
+# per-rank shares of a multiple of 4 jobs take the 8-byte-load passes; 3002 (1501 per rank) the 2-byte ones
+@pytest.mark.parametrize("n,k,levels", [(3000, 16, 7), (640, 64, 1000), (3002, 16, 7)])
 def test_sharded_auction_gpu_passes_two_ranks(n, k, levels):
     """Two ranks on one GPU (gloo collectives over device tensors), each running the rqsid_dauction_*
     passes on its row block: the concatenation equals the single-process GPU auction (pinned to the
