@@ -80,6 +80,8 @@ struct SegAuction {
   uint32_t* above;               // [n_multi*K][kAbovePad] values with high byte > b1 (one line per worker:
                                  // every chunk block adds to it)
   uint8_t* miss;                 // [n_multi*K]
+  uint16_t* chist;               // [total_chunks][K][256] each chunk's low-byte histogram of bin b1 from the
+                                 // guessed pass: a hit worker's per-chunk tie count is entry T & 255
 };
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ off, int n_seg, int64_t i) {
@@ -353,6 +355,13 @@ __global__ __launch_bounds__(256) void sa_hist_kernel(SegAuction a) {
   }
   __syncthreads();
   if (MODE == 2 && threadIdx.x < nw && abv[threadIdx.x]) atomicAdd(&a.above[(hw0 + threadIdx.x) * kAbovePad], abv[threadIdx.x]);
+  if (MODE == 2) {  // counts <= kCh fit 16 bits; one 8-byte store per 4 slots
+    uint16_t* dst = a.chist + ((int64_t)blockIdx.x * a.K + w0) * 256;
+    for (int i = threadIdx.x; i < nw * 64; i += 256) {
+      const uint32_t* q = &h[0][0] + 4 * i;
+      *reinterpret_cast<uint2*>(dst + 4 * i) = make_uint2(q[0] | (q[1] << 16), q[2] | (q[3] << 16));
+    }
+  }
   for (int i = threadIdx.x; i < nw * 256; i += 256) {
     const uint32_t c = (&h[0][0])[i];  // zero for the workers that did not take part
     if (c) atomicAdd(&a.hist[(hw0 + i / 256) * 256 + (i & 255)], c);
@@ -486,6 +495,12 @@ __global__ __launch_bounds__(256) void sa_eqcount_kernel(SegAuction a) {
   __shared__ uint32_t c[kKG];
   const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
   const int64_t sw0 = (int64_t)ci.s * a.K + w0;
+  if (a.chist) {  // hit workers take their counts from the guessed pass's chunk histograms (eqscan)
+    const int64_t hw0 = (int64_t)a.hidx[ci.s] * a.K + w0;
+    bool any = false;
+    for (int g = 0; g < nw; ++g) any |= a.miss[hw0 + g] != 0;
+    if (!any) return;
+  }
   if (threadIdx.x < kKG) c[threadIdx.x] = 0;
   __syncthreads();
   _Float16 vT[kKG];
@@ -520,10 +535,14 @@ __global__ __launch_bounds__(256) void sa_eqscan_kernel(SegAuction a) {
   const int lane = threadIdx.x & 63;
   uint32_t* e = a.eqcnt + (int64_t)w * a.total_chunks;
   const int64_t c0 = a.chunk_off[s], c1 = a.chunk_off[s + 1];
+  // a worker the guessed pass found (T in last round's bin): its chunk counts of T are entries of the
+  // chunk histograms; a missed worker's come from sa_eqcount_kernel
+  const bool from_hist = a.chist && !a.miss[hw];
+  const uint16_t* ch = from_hist ? a.chist + (int64_t)w * 256 + (a.sel[((int64_t)s * a.K + w) * 4 + 2] & 255u) : nullptr;
   uint32_t carry = 0;
   for (int64_t base = c0; base < c1; base += 64) {
     const int64_t i = base + lane;
-    const uint32_t v = i < c1 ? e[i] : 0;
+    const uint32_t v = i < c1 ? (from_hist ? (uint32_t)ch[i * a.K * 256] : e[i]) : 0;
     uint32_t x = v;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y = (uint32_t)__shfl_up((int)x, o);
@@ -755,6 +774,7 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.eqtot = c.take<uint32_t>((int64_t)S * K);
   a.above = guess ? c.take<uint32_t>((int64_t)a.n_multi * K * kAbovePad) : nullptr;
   a.miss = guess ? c.take<uint8_t>((int64_t)a.n_multi * K) : nullptr;
+  a.chist = guess && a.n_multi > 0 ? c.take<uint16_t>(total_chunks * K * 256) : nullptr;
 }
 
 }  // namespace
