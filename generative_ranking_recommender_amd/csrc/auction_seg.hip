@@ -14,7 +14,10 @@
 // Jobs are cut into chunks of kCh jobs that never straddle segments (seg_chunk_off = exclusive scan of
 // ceil(N_s / kCh)).  A segment of one chunk (the last layer's groups: median ~600 rows) selects its
 // per-worker thresholds inside one block from LDS histograms (sa_small_select_kernel); wider segments
-// (the middle layer's parents) use per-(segment, worker) global histograms like auction.hip.
+// (the middle layer's parents, and the single auction of auction.hip) use per-(segment, worker) global
+// histograms.  A round of a wide segment is two sweeps of W when each worker's threshold stays in last
+// round's high-byte bin (guessed pass with its per-chunk tie counts, then the bids); a worker whose
+// threshold left the bin takes the exact two-pass selection and a tie-count sweep in the same round.
 #include <algorithm>
 #include <cmath>
 
