@@ -55,6 +55,8 @@ SIGNATURES = {
     "rqsid_auction_scores": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "rqsid_auction_workspace_bytes": (c_i64, [c_i64, c_i32]),
     "rqsid_auction_lap_half": (c_i32, [c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "rqsid_auction_full_workspace_bytes": (c_i64, [c_i64, c_i32]),
+    "rqsid_auction_lap_full": (c_i32, [c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "rqsid_seg_auction_scores": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_i32, c_vp, c_vp, c_i64, c_i32, c_vp,
                                          c_vp]),
     "rqsid_seg_auction_chunk_jobs": (c_i32, []),

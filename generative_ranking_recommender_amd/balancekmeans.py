@@ -70,9 +70,19 @@ def auction_lap_half(job_and_worker_to_score: torch.Tensor, return_token_to_work
 
 
 def auction_lap_full(job_and_worker_to_score: torch.Tensor, return_token_to_worker: bool = True):
-    """balancekmeans/__init__.py:142-210 is only reachable through predict(balanced=True), which no
-    caller uses."""
-    raise NotImplementedError("auction_lap_full (predict(balanced=True)) is not on the semantic-ID path")
+    """balancekmeans/__init__.py:142-210: the fp32 auction (``rqsid_auction_lap_full``), reached through
+    ``KMeans.predict(balanced=True)`` (:523-525).  Returns the worker of every job (int64, on the scores'
+    device), like the reference with return_token_to_worker=True."""
+    s = job_and_worker_to_score
+    if not return_token_to_worker:
+        raise NotImplementedError("return_token_to_worker=False is unused by the reference's callers")
+    dev = s.device if s.device.type == "cuda" else _device(None)
+    if torch.isnan(s).any():
+        raise Exception("NaN distance")  # :152-154
+    w = s.to(dev).float().t().contiguous()
+    a, rounds = ops.auction_full(w)
+    logger.debug("auction_lap_full: %d jobs, %d workers, %d rounds", s.shape[0], s.shape[1], rounds)
+    return a.long()
 
 
 class KMeans:
@@ -188,14 +198,17 @@ class KMeans:
 
     def predict(self, X, distance="euclidean", gamma_for_soft_dtw=0.001, tqdm_flag=False, return_distances=False,
                 balanced=False):
-        """:489-534 — nearest centre (exact argmin, lowest index on ties); int64 on the CPU."""
+        """:489-534 — nearest centre (exact argmin, lowest index on ties); with balanced=True the fp32
+        auction on -distance (:523-525).  int64 on the CPU."""
         self._check_distance(distance)
-        if balanced:
-            raise NotImplementedError("predict(balanced=True) uses auction_lap_full, unused by the reference's callers")
         X = _to_dev(X, self.device)
         if X.dim() == 1:
             X = X.unsqueeze(0)
         c = self.cluster_centers.float().to(self.device).contiguous()
+        if balanced:
+            d = ops.pairwise_distance(X, c)
+            ids = auction_lap_full(-d).cpu()
+            return (ids, d) if return_distances else ids
         ids = ops.nearest(X, ops.prepare_centers(c)).long().cpu()
         if return_distances:
             return ids, ops.pairwise_distance(X, c)

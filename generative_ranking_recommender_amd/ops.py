@@ -331,6 +331,23 @@ def auction(scores_wj: torch.Tensor, max_rounds: int = 0):
     return out, int(rounds.value)
 
 
+def auction_full(scores_wj: torch.Tensor, max_rounds: int = 0):
+    """fp32 balanced assignment on worker-major scores [K][N] (include/rqsid.h rqsid_auction_lap_full).
+    Returns (assignment i32[N], rounds)."""
+    scores_wj = scores_wj.to(torch.float32).contiguous()
+    _require_device(scores_wj)
+    k, n = scores_wj.shape
+    out = torch.empty(n, dtype=torch.int32, device=scores_wj.device)
+    if n == 0:
+        return out, 0
+    wsb = int(lib().rqsid_auction_full_workspace_bytes(n, k))
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=scores_wj.device)
+    rounds = ctypes.c_int32(0)
+    _lib.check(lib().rqsid_auction_lap_full(_ptr(scores_wj), k, n, int(max_rounds), _ptr(out), ctypes.addressof(rounds),
+                                            _ptr(ws), wsb, _stream()), "rqsid_auction_lap_full")
+    return out, int(rounds.value)
+
+
 def greedy_match(dist: torch.Tensor, sub_off: torch.Tensor, max_take: int):
     """Greedy unique-nearest columns per group (see include/rqsid.h rqsid_greedy_match).
     dist: f32 [total_sub, C]; sub_off: i32 [G+1].  Returns (match u8 [G, C], n_selected i32 [G])."""

@@ -177,6 +177,17 @@ int rqsid_auction_lap_half(const uint16_t* scores_wj, int32_t n_workers, int64_t
                            int32_t max_rounds, int32_t* out_assign, int32_t* out_rounds,
                            void* workspace, int64_t workspace_bytes, void* stream);
 
+/* The fp32 auction of balancekmeans.auction_lap_full (balancekmeans/__init__.py:142-210), reached only
+ * through KMeans.predict(balanced=True) (:523-525), on fp32 scores scores_wj[K][N] (worker-major).
+ * Every fp32 operation of the reference with one rounding; the same tie rules as rqsid_auction_lap_half.
+ * Unlike auction_lap_half it has no N < K fallback: with jobs_per_worker = 0 nothing bids until the
+ * leftover rule gives every job to worker 0 after round 1000.  Blocks the calling thread (one host read
+ * per round); *out_rounds = rounds run.  N >= 1, 2 <= K <= 65535. */
+int64_t rqsid_auction_full_workspace_bytes(int64_t n_jobs, int32_t n_workers);
+int rqsid_auction_lap_full(const float* scores_wj, int32_t n_workers, int64_t n_jobs, int32_t max_rounds,
+                           int32_t* out_assign, int32_t* out_rounds, void* workspace, int64_t workspace_bytes,
+                           void* stream);
+
 /* Segmented auction scores for many independent balanced fits at once (the per-parent sub-K-Means of
  * hierarchical_rq_kmeans.py:671-752 and the per-group sub-K-Means of :968-1053, which the reference runs
  * one after another, each through balancekmeans/__init__.py:29-43,536-603).  Segment s owns rows

@@ -272,6 +272,60 @@ def auction_lap_half(job_and_worker_to_score: np.ndarray, tie_rule: str = "torch
         counter += 1
 
 
+def auction_lap_full(job_and_worker_to_score: np.ndarray, tie_rule: str = "torch") -> np.ndarray:
+    """balancekmeans/__init__.py:142-210 (return_token_to_worker=True): the fp32 auction, reached only
+    through ``KMeans.predict(balanced=True)`` (:523-525).  Same steps as ``auction_lap_half`` in fp32, with
+    one rounding per op, and two differences of the reference: no N < K fallback (with jobs_per_worker
+    = 0 nothing bids until the leftover rule gives every job to worker 0 after round 1000), and eps from
+    the fp32 spread.  ``tie_rule`` as in ``auction_lap_half``."""
+    s = np.asarray(job_and_worker_to_score, dtype=F32)
+    num_jobs, num_workers = s.shape
+    eps = F32(F32(s.max() - s.min()) / F32(50.0))
+    eps = max(eps, F32(1e-4))
+    if np.isnan(s).any():
+        raise Exception("NaN distance")
+    w = np.ascontiguousarray(s.T)  # [workers, jobs]
+    jpw = num_jobs // num_workers
+    value = w.copy()
+    cost = np.zeros(num_jobs, dtype=F32)
+    counter = 0
+    index = None
+    jobs_without_bidder = None
+    if tie_rule == "torch":
+        import torch
+    while True:
+        if tie_rule == "torch":
+            tv, ti = torch.from_numpy(value).topk(jpw + 1, dim=1)
+            top_index = ti.numpy()
+        else:
+            order = np.lexsort((np.arange(num_jobs)[None, :].repeat(num_workers, 0), -value), axis=1)
+            top_index = order[:, :jpw + 1]
+        top_values = np.take_along_axis(value, top_index, 1)
+        inc = (top_values[:, :-1] - top_values[:, -1:]) + eps
+        bids = np.zeros((num_workers, num_jobs), dtype=F32)
+        np.put_along_axis(bids, top_index[:, :-1], inc, 1)
+        if counter < 100 and index is not None:
+            bids.reshape(-1)[index] = eps
+        if counter > 1000:
+            bids.reshape(-1)[jobs_without_bidder] = eps
+        jobs_with_bidder = np.nonzero((bids > 0).any(0))[0]
+        jobs_without_bidder = np.nonzero((bids == 0).all(0))[0]
+        sub = bids[:, jobs_with_bidder]
+        if tie_rule == "torch":
+            hb, hbr = torch.from_numpy(np.ascontiguousarray(sub)).max(dim=0)
+            high_bidders, high_bids = hbr.numpy(), hb.numpy()
+        else:
+            high_bidders = sub.argmax(0)
+            high_bids = sub[high_bidders, np.arange(len(jobs_with_bidder))]
+        if len(high_bidders) == num_jobs:
+            return high_bidders.astype(np.int64)
+        cost[jobs_with_bidder] += high_bids
+        value = w - cost[None, :]
+        index = high_bidders * num_jobs + jobs_with_bidder
+        value.reshape(-1)[index] = w.reshape(-1)[index]
+        counter += 1
+
+
 class LegacyRNG:
     """The reference draws init indices from numpy's global legacy RNG (np.random.choice,
     balancekmeans/__init__.py:250-253) and empty-cluster rows from torch's CPU RNG."""

@@ -144,6 +144,21 @@ def g_auction():
     save("auction", **res)
 
 
+# --- G5b: auction_lap_full (fp32; only predict(balanced=True) reaches it) -------
+def g_auction_full():
+    res = {}
+    cases = {"n64k8": (64, 8, 17), "n67k8": (67, 8, 18), "n1000k16": (1000, 16, 19),
+             "n5k8": (5, 8, 20), "n96k8": (96, 8, 21)}
+    for tag, (n, k, seed) in cases.items():
+        X = synth.small_mixture(n, d=32, m=6, seed=seed)
+        C = synth.small_mixture(k, d=32, m=6, seed=seed + 100)
+        dist = ref_bk.pairwise_distance_full(torch.from_numpy(X), torch.from_numpy(C))
+        out = ref_bk.auction_lap_full(-dist)
+        res[f"dist_{tag}"] = dist.numpy()
+        res[f"out_{tag}"] = out.numpy().astype(np.int64)
+    save("auction_full", **res)
+
+
 # --- G6: fit_by_min_loss / fit (balanced) trajectories ----------------------
 def g_fit():
     X = synth.small_mixture(512, m=16, seed=23)

@@ -8,7 +8,8 @@ import torch
 
 from generative_ranking_recommender_amd import ops, synth
 from generative_ranking_recommender_amd import io as rq_io
-from generative_ranking_recommender_amd.balancekmeans import KMeans, auction_lap_half, pairwise_distance_half
+from generative_ranking_recommender_amd.balancekmeans import (KMeans, auction_lap_half, pairwise_distance_full,
+                                                              pairwise_distance_half)
 from generative_ranking_recommender_amd.hierarchical_rq_kmeans import HierarchicalRQKMeans, HierarchicalRQKMeansConfig
 from generative_ranking_recommender_amd.simplified_semantic_id_generator import SimplifiedHierarchicalRQ
 from oracle import rq_oracle as O
@@ -49,6 +50,38 @@ def test_auction_random_and_tied_match_oracle(n, k, levels):
     assert (got == ref).all()
     if n % k:
         assert rounds == 1002  # the leftover rule ends it (Appendix A item 6)
+
+
+@pytest.mark.parametrize("tag", ["n64k8", "n67k8", "n1000k16", "n5k8", "n96k8"])
+def test_auction_full_golden_inputs_match_reference(golden, tag):
+    """fp32 auction (auction_lap_full, A6) on the reference's own outputs (tests/golden/auction_full.npz,
+    captured by running the reference: 1002-round leftover case n67k8, N < K case n5k8)."""
+    g = golden("auction_full")
+    dist, want = _data.auction_case(g, tag)
+    got, _ = ops.auction_full(torch.from_numpy(np.ascontiguousarray(-dist.T)).to(DEV))
+    assert (got.cpu().numpy() == want).all()
+
+
+@pytest.mark.parametrize("n,k,levels", [(300, 8, 0), (2050, 16, 5), (999, 16, 7), (40, 32, 3)])
+def test_auction_full_random_and_tied_match_oracle(n, k, levels):
+    rng = np.random.default_rng(n * k + 1)
+    d = rng.random((n, k), dtype=np.float32) * 4
+    if levels:
+        d = np.round(d * levels) / levels  # heavy ties at every top-k boundary
+    s = -d
+    got, rounds = ops.auction_full(torch.from_numpy(np.ascontiguousarray(s.T)).to(DEV))
+    assert (got.cpu().numpy() == O.auction_lap_full(s, tie_rule="stable")).all()
+    if n % k:
+        assert rounds == 1002
+
+
+def test_kmeans_predict_balanced_uses_fp32_auction():
+    x = torch.from_numpy(synth.small_mixture(512, m=8, seed=4)).to(DEV)
+    km = KMeans(n_clusters=8, cluster_centers=x[:8].clone(), device=DEV)
+    got = km.predict(x, balanced=True).numpy()
+    d = pairwise_distance_full(x, x[:8].clone()).cpu().numpy()
+    assert (got == O.auction_lap_full(-d, tie_rule="stable")).all()
+    assert np.bincount(got, minlength=8).max() <= 512 // 8
 
 
 def test_auction_fewer_jobs_than_workers_is_farthest():

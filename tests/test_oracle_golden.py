@@ -69,6 +69,15 @@ def test_auction_matches_reference(golden, tag):
     assert (got == out).all()
 
 
+@pytest.mark.parametrize("tag", ["n64k8", "n67k8", "n1000k16", "n5k8", "n96k8"])
+@pytest.mark.parametrize("tie_rule", ["torch", "stable"])
+def test_auction_full_matches_reference(golden, tag, tie_rule):
+    """oracle auction_lap_full (fp32) == the reference's auction_lap_full outputs (tests/golden)."""
+    g = golden("auction_full")
+    dist, out = _data.auction_case(g, tag)
+    assert (O.auction_lap_full(-dist, tie_rule=tie_rule) == out).all()
+
+
 def test_kmeans_drivers_match_reference(golden):
     g = golden("fit")
     x = _data.fit_inputs(g)
