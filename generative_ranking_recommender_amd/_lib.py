@@ -7,9 +7,12 @@ repository snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import fcntl
 import os
 import subprocess
+import tempfile
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -93,41 +96,63 @@ _lib = None
 _io_lib = None
 
 
+def _stale(lib: Path, deps) -> bool:
+    return not lib.exists() or lib.stat().st_mtime < max(f.stat().st_mtime for f in deps)
+
+
+@contextlib.contextmanager
+def _build_lock():
+    """One builder at a time (torchrun ranks or test workers may all find the library stale)."""
+    lockdir = PKG / "build"
+    lockdir.mkdir(exist_ok=True)
+    with open(lockdir / ".lock", "w") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(f, fcntl.LOCK_UN)
+
+
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile the HIP library for gfx950 (hipcc cross-compiles without a GPU)."""
-    if LIB_PATH.exists() and not force and LIB_PATH.stat().st_mtime >= max(f.stat().st_mtime for f in DEPS + [HEADER]):
+    if not force and not _stale(LIB_PATH, DEPS + [HEADER]):
         return LIB_PATH
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    tmp = LIB_PATH.with_suffix(".so.tmp")
-    objdir = PKG / "build"
-    objdir.mkdir(exist_ok=True)
-    compile_flags = [f for f in HIPCC_FLAGS if f != "-shared"]
-    objs = [objdir / (src.stem + ".o") for src in SRCS]
-    cmds = [[hipcc, *compile_flags, "-c", "-o", str(o), str(src)] for src, o in zip(SRCS, objs)]
-    if verbose:
-        for c in cmds:
-            print(" ".join(c))
-    # one hipcc per translation unit, in parallel (the kernels are template-heavy: minutes serially)
-    procs = [subprocess.Popen(c) for c in cmds]
-    bad = [c for c, pr in zip(cmds, procs) if pr.wait() != 0]
-    if bad:
-        raise subprocess.CalledProcessError(1, bad[0])
-    subprocess.run([hipcc, *HIPCC_FLAGS, "-o", str(tmp), *map(str, objs)], check=True)
-    os.replace(tmp, LIB_PATH)
+    with _build_lock():
+        if not force and not _stale(LIB_PATH, DEPS + [HEADER]):
+            return LIB_PATH  # another process built it while this one waited
+        compile_flags = [f for f in HIPCC_FLAGS if f != "-shared"]
+        with tempfile.TemporaryDirectory(dir=PKG / "build") as objdir:
+            objs = [Path(objdir) / (src.stem + ".o") for src in SRCS]
+            cmds = [[hipcc, *compile_flags, "-c", "-o", str(o), str(src)] for src, o in zip(SRCS, objs)]
+            if verbose:
+                for c in cmds:
+                    print(" ".join(c))
+            # one hipcc per translation unit, in parallel (the kernels are template-heavy: minutes serially)
+            procs = [subprocess.Popen(c) for c in cmds]
+            bad = [c for c, pr in zip(cmds, procs) if pr.wait() != 0]
+            if bad:
+                raise subprocess.CalledProcessError(1, bad[0])
+            tmp = Path(objdir) / LIB_PATH.name
+            subprocess.run([hipcc, *HIPCC_FLAGS, "-o", str(tmp), *map(str, objs)], check=True)
+            os.replace(tmp, LIB_PATH)
     return LIB_PATH
 
 
 def build_io(force: bool = False, verbose: bool = False) -> Path:
     """Compile the host I/O library (g++)."""
-    if (IO_LIB_PATH.exists() and not force
-            and IO_LIB_PATH.stat().st_mtime >= max(f.stat().st_mtime for f in IO_SRCS + [IO_HEADER])):
+    if not force and not _stale(IO_LIB_PATH, IO_SRCS + [IO_HEADER]):
         return IO_LIB_PATH
-    tmp = IO_LIB_PATH.with_suffix(".so.tmp")
-    cmd = [os.environ.get("CXX", "g++"), *IO_FLAGS, "-o", str(tmp), *map(str, IO_SRCS)]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, IO_LIB_PATH)
+    with _build_lock():
+        if not force and not _stale(IO_LIB_PATH, IO_SRCS + [IO_HEADER]):
+            return IO_LIB_PATH
+        with tempfile.TemporaryDirectory(dir=PKG / "build") as d:
+            tmp = Path(d) / IO_LIB_PATH.name
+            cmd = [os.environ.get("CXX", "g++"), *IO_FLAGS, "-o", str(tmp), *map(str, IO_SRCS)]
+            if verbose:
+                print(" ".join(cmd))
+            subprocess.run(cmd, check=True)
+            os.replace(tmp, IO_LIB_PATH)
     return IO_LIB_PATH
 
 

@@ -224,7 +224,8 @@ def init_indices(num_samples: int, n_clusters: int) -> np.ndarray:
 
 
 def batched_fit(X: torch.Tensor, layout: "ops.SegmentLayout", n_clusters: int, iter_limits, inits,
-                target_nodes_num=None, tol: float = 1e-3, half: bool = False, balanced: bool = True):
+                target_nodes_num=None, tol: float = 1e-3, half: bool = False, balanced: bool = True,
+                return_info: bool = False):
     """Many independent K-Means fits advanced in lockstep, one per segment of the segment-ordered rows X
     (segment s = rows layout.off[s] .. layout.off[s+1]), each exactly the iteration of KMeans.fit
     (:368-465; ``target_nodes_num`` None) or KMeans.fit_by_min_loss (:259-365; re-initialised every 10
@@ -241,7 +242,10 @@ def batched_fit(X: torch.Tensor, layout: "ops.SegmentLayout", n_clusters: int, i
     exactly the reference's draws.  Empty clusters take a random row of their segment from the global
     torch RNG, drawn in (iteration, segment, cluster) order.
 
-    Returns (centres f32 [S*K, D], last assignment i32 [N] local to each segment)."""
+    Returns (centres f32 [S*K, D], last assignment i32 [N] local to each segment); with ``return_info``
+    also {"iterations": i64[S] iterations run per segment, "events": [(segment, iteration), ...] the
+    empty-cluster torch draws in the order they were made}.  ``fit_segments`` uses both to prove (or
+    restore) the reference's sequential RNG consumption."""
     dev = X.device
     S, K = layout.n_seg, n_clusters
     off = layout.off
@@ -266,6 +270,7 @@ def batched_fit(X: torch.Tensor, layout: "ops.SegmentLayout", n_clusters: int, i
         buckets = ops.bucket(seg_row, S)
         cand = ops.contiguous_candidates(S, K, dev)
     rows_of = torch.arange(S * K, device=dev).view(S, K)
+    events = []
     while active.any():
         if min_loss_mode:
             re = np.nonzero(active & (iteration > 0) & (iteration % 10 == 0))[0]
@@ -289,6 +294,7 @@ def batched_fit(X: torch.Tensor, layout: "ops.SegmentLayout", n_clusters: int, i
         for s in np.nonzero(active)[0]:
             for k in np.nonzero(cnt[s] == 0)[0]:
                 new[s * K + k] = X[int(off[s]) + int(torch.randint(int(layout.sizes[s]), (1,)).item())]
+                events.append((int(s), int(iteration[s])))
         frozen = torch.from_numpy(~active).to(dev)
         new[frozen.repeat_interleave(K)] = prev[frozen.repeat_interleave(K)]
         centers = new.contiguous()
@@ -305,4 +311,98 @@ def batched_fit(X: torch.Tensor, layout: "ops.SegmentLayout", n_clusters: int, i
         iteration[active] += 1
         done = active & ((shift.astype(np.float64) ** 2 < tol) | ((limits != 0) & (iteration >= limits)))
         active &= ~done
-    return (best if min_loss_mode else centers), last[:layout.n]
+    out = (best if min_loss_mode else centers), last[:layout.n]
+    if return_info:
+        return out + ({"iterations": iteration.copy(), "events": events},)
+    return out
+
+
+def reinit_draws(iter_limit: int) -> int:
+    """Initialisation draws of a fit_by_min_loss run of ``iter_limit`` iterations: its start plus one
+    re-initialisation at every iteration 10, 20, ... it reaches (balancekmeans/__init__.py:295, 305-306)."""
+    return 1 + max(0, (int(iter_limit) - 1) // 10)
+
+
+def fit_segments(X: torch.Tensor, sizes, n_clusters: int, iter_limits, inits=None, target_nodes_num=None,
+                 tol: float = 1e-3, half: bool = False, max_restarts: int = 3):
+    """The reference's one-after-another sub-fits (hierarchical_rq_kmeans.py:703-731, 1010-1019;
+    simplified_semantic_id_generator.py:119-133, 275-278) run in lockstep by ``batched_fit``, with the
+    reference's random-number consumption restored exactly.
+
+    X holds the segments' rows in segment order (segment s = the next sizes[s] rows).  Two schedules
+    of the reference cannot be known before a fit has run:
+    * numpy: ``fit_by_min_loss`` draws a re-initialisation at iteration 10, 20, ... only while it has
+      not converged.  With ``target_nodes_num`` set, every segment's start and every re-initialisation
+      its budget allows are drawn here, speculatively, in segment order.
+    * torch: an empty cluster draws ``torch.randint(len(X), (1,))`` (:321-322); the lockstep loop draws
+      in (iteration, segment) order, the reference in (segment, iteration) order.
+    After each lockstep run the first segment whose draws differ from the reference's is found (one that
+    converged early with unused re-initialisations: the segments after it; a torch draw taken out of the
+    reference's order: that segment).  Segments before it are exact and kept; the generators are put in
+    the reference's state at that point (numpy: re-drawn from the saved state; torch: the exact draws
+    replayed) and the remaining segments run again.  After ``max_restarts`` such restarts the rest runs
+    one segment at a time, which is exact by construction.  Without ``target_nodes_num`` (``fit``) the
+    caller draws the starts (``inits[s] = [indices]``) in its own order, interleaved with its other draws.
+
+    Returns (centres f32 [S*K, D], last assignment i32 [N] local to each segment)."""
+    dev = X.device
+    sizes = np.asarray(sizes, dtype=np.int64)
+    S, K = len(sizes), n_clusters
+    limits = np.asarray(iter_limits, dtype=np.int64).reshape(S)
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    min_loss_mode = target_nodes_num is not None
+    if min_loss_mode and (limits == 0).any():
+        raise ValueError("fit_segments: fit_by_min_loss needs a finite iter_limit per segment")
+    if not min_loss_mode and (inits is None or len(inits) != S):
+        raise ValueError("fit_segments: fit needs each segment's drawn start")
+    centers = torch.empty((S * K, X.shape[1]), dtype=torch.float32, device=dev)
+    last = torch.empty((max(int(off[-1]), 1),), dtype=torch.int32, device=dev)
+    torch_state = torch.get_rng_state()
+    start, restarts = 0, 0
+    while start < S:
+        stop = S if restarts <= max_restarts else start + 1
+        segs = range(start, stop)
+        np_states, seg_inits = [], []
+        for s in segs:
+            if min_loss_mode:
+                np_states.append(np.random.get_state())
+                seg_inits.append([init_indices(int(sizes[s]), K) for _ in range(reinit_draws(limits[s]))])
+            else:
+                seg_inits.append(inits[s])
+        torch.set_rng_state(torch_state)
+        layout = ops.SegmentLayout(sizes[start:stop], dev)
+        xs = X[int(off[start]):int(off[stop])].contiguous()
+        c, a, info = batched_fit(xs, layout, K, limits[start:stop], seg_inits, target_nodes_num=target_nodes_num,
+                                 tol=tol, half=half, return_info=True)
+        # numpy: the first segment that drew re-initialisations it never used
+        bad_np, used = stop, None
+        if min_loss_mode:
+            for i in range(stop - start):
+                u = reinit_draws(max(int(info["iterations"][i]), 1))
+                if u < len(seg_inits[i]):
+                    bad_np, used = start + i, u
+                    break
+        # torch: the first segment with a draw outside the reference's (segment, iteration) order
+        ev = [start + e[0] for e in info["events"]]
+        ref = sorted(range(len(ev)), key=lambda t: ev[t])
+        wrong = [ev[t] for p, t in enumerate(ref) if t != p]
+        bad_torch = min(wrong) if wrong else stop
+        good = min(bad_np + 1, bad_torch, stop)
+        centers[start * K:good * K] = c[:(good - start) * K]
+        last[int(off[start]):int(off[good])] = a[:int(off[good] - off[start])]
+        # the generators' state after the kept segments, as the reference leaves it
+        if min_loss_mode:
+            if good == bad_np + 1:
+                np.random.set_state(np_states[bad_np - start])
+                for _ in range(used):
+                    init_indices(int(sizes[bad_np]), K)
+            elif good < stop:
+                np.random.set_state(np_states[good - start])
+        torch.set_rng_state(torch_state)
+        for seg in sorted(e for e in ev if e < good):
+            torch.randint(int(sizes[seg]), (1,))
+        torch_state = torch.get_rng_state()
+        if good < stop:
+            restarts += 1
+        start = good
+    return centers, last[:int(off[-1])]

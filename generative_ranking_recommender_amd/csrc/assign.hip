@@ -1059,6 +1059,9 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
                       (res_levels != 1 || !norm || den_out);
   const bool use_res = res_ok && variant == 6;
   if (use_res) {
+    p.err = p.work_count + 48;  // zeroed with the workspace header above
+    const char* fc = getenv("RQSID_TEST_FORCE_SPIN_CAP");
+    p.force_cap = fc && atoi(fc) ? 1 : 0;
     int4* desc = reinterpret_cast<int4*>(work_idx + (n_rows * 4 + 255) / 256 * 64);
     // tile_seg's slot holds the segment of each ambiguous row
     if ((rc = launch_resident_screen(p, t3, res_levels, norm, desc, work_idx, tile_seg, n_rows, st))) return rc;
@@ -1096,7 +1099,16 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   else if (res_levels == 1) hipLaunchKernelGGL((assign_rescore_kernel<1, false>), g, dim3(256), 0, st, p);
   else if (norm) hipLaunchKernelGGL((assign_rescore_kernel<2, true>), g, dim3(256), 0, st, p);
   else hipLaunchKernelGGL((assign_rescore_kernel<2, false>), g, dim3(256), 0, st, p);
-  return check_launch("assign_rescore");
+  if ((rc = check_launch("assign_rescore"))) return rc;
+  if (use_res) {
+    // the resident screen's role waits are capped (assign_resident.hip): a wave that gave up waiting
+    // left wrong IDs behind, so the call fails instead of returning them (one readback, opt-in path)
+    int32_t err = 0;
+    if (hipMemcpyAsync(&err, p.err, 4, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+      return fail(RQSID_E_LAUNCH, "assign: error word readback");
+    if (err) return fail(RQSID_E_LAUNCH, "assign: a resident-screen wait reached its spin cap (error word %d)", err);
+  }
+  return RQSID_OK;
 }
 
 #ifdef RQSID_STAMPS

@@ -67,6 +67,8 @@ struct AssignParams {
   const int32_t* seg_cb;
   const float* den_in;
   float* den_out;
+  int32_t* err;           // device error word (resident screen: bit 0 = a role wait reached its spin cap)
+  int32_t force_cap;      // tests only: the resident screen's final wait takes a zero spin cap
 };
 
 __device__ __forceinline__ int cand_global(const AssignParams& p, int base, int local) {

@@ -199,16 +199,18 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // are untouched (no fence): the roles exchange LDS data only.
 constexpr int kSpinCap = 1 << 20;  // ~0.1 s: far beyond any legitimate wait
 // ``dead`` (wave-uniform): set by a wait that reached the cap; later waits of the wave return at once,
-// so even a broken protocol ends the kernel in about one capped wait per wave (with wrong results)
+// so even a broken protocol ends the kernel in about one capped wait per wave.  Its results would be
+// wrong: every wave that went dead sets bit 0 of the device error word p.err at its exit, and
+// rqsid_assign reads the word back and returns RQSID_E_LAUNCH (never wrong IDs silently).
 __device__ __forceinline__ void lds_publish(uint32_t* own, uint32_t count) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   *reinterpret_cast<volatile uint32_t*>(own) = count;
   asm volatile("" ::: "memory");
 }
 template <int N>  // N = 4 or 8 counters, 16-B aligned
-__device__ __forceinline__ void lds_wait_all(const uint32_t* ctr, uint32_t target, int& dead) {
-  int spin = dead ? kSpinCap : 0;
-  for (; spin < kSpinCap; ++spin) {
+__device__ __forceinline__ void lds_wait_all(const uint32_t* ctr, uint32_t target, int& dead, int cap = kSpinCap) {
+  int spin = dead ? cap : 0;
+  for (; spin < cap; ++spin) {
     asm volatile("" ::: "memory");
     const volatile uint32_t* c = ctr;
     uint32_t m = c[0];
@@ -217,7 +219,7 @@ __device__ __forceinline__ void lds_wait_all(const uint32_t* ctr, uint32_t targe
     if ((uint32_t)runi((int)m) >= target) break;
     __builtin_amdgcn_s_sleep(1);
   }
-  dead = spin >= kSpinCap ? 1 : dead;
+  dead = spin >= cap ? 1 : dead;
   asm volatile("" ::: "memory");
 }
 
@@ -770,10 +772,11 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
     const int nt = te - tb;
     lds_publish(ctr_posted + cw, (uint32_t)(nt + 1));
     if (cw == (nt & (kCW - 1))) {
-      lds_wait_all<kCW>(ctr_posted, (uint32_t)(nt + 1), dead);
+      lds_wait_all<kCW>(ctr_posted, (uint32_t)(nt + 1), dead, p.force_cap ? 0 : kSpinCap);
       store_masks(prev_row, prev_amb, (nt - 1) & 1);
     }
   }
+  if (dead && lane == 0) atomicOr(p.err, 1);
 #ifdef RQSID_STAMPS
   RS(rs_acc[7] = (uint32_t)(te - tb);)
   if (lane == 0 && (wave == 0 || wave == kCW)) {

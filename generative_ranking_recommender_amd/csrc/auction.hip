@@ -216,6 +216,16 @@ int rqsid_auction_lap_full(const float* scores_wj, int32_t n_workers, int64_t n_
   if (!workspace || workspace_bytes < full_ws(n_jobs)) return fail(RQSID_E_WORKSPACE, "auction_full: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   if (out_rounds) *out_rounds = 0;
+  if (n_jobs < n_workers) {
+    // jobs_per_worker = 0: topk(1) leaves no bid increments, so nothing bids until the leftover rule
+    // (:182-183) hands every job to worker 0 in round 1002.  The result is known without the rounds.
+    if (max_rounds > 0 && max_rounds < 1002)
+      return fail(RQSID_E_LAUNCH, "auction_full: no complete assignment after %d rounds", max_rounds);
+    if (hipMemsetAsync(out_assign, 0, (size_t)n_jobs * 4, st) != hipSuccess)
+      return fail(RQSID_E_LAUNCH, "auction_full: memset");
+    if (out_rounds) *out_rounds = 1002;
+    return RQSID_OK;
+  }
   auto al = [](int64_t b) { return (b + 255) / 256 * 256; };
   char* p = (char*)workspace;
   FullAuction a{};

@@ -194,6 +194,7 @@ __global__ __launch_bounds__(256) void sa_seg_init_kernel(SegAuction a, const ui
   uint8_t f = 0;
   // live: requested, non-empty, and N_s >= K (N_s < K takes the argmin fallback, 0 rounds)
   if ((!active || active[s]) && n_s > 0 && n_s >= a.K) f |= kLive;
+  if ((f & kLive) && a.live_count) atomicAdd(a.live_count, 1u);
   if (nch == 1 && !a.n_glob) f |= kSingle;
   a.flag[s] = f;
   a.mm[2 * s] = 0;
@@ -838,34 +839,35 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   Carve c{(char*)workspace};
   carve(a, c, n_jobs, n_workers, n_seg, total_chunks, true);
   const unsigned gs = (unsigned)cdiv(n_seg, 256);
-  uint32_t* host = nullptr;  // pinned readback: [0] live segments, [1] multi-chunk segments
-  if (hipHostMalloc((void**)&host, 2 * sizeof(uint32_t)) != hipSuccess)
+  // pinned readback ([0] live segments, [1] multi-chunk segments): one buffer per host thread, kept
+  // for the thread's lifetime (the lockstep fits call this once per iteration)
+  static thread_local uint32_t* host = nullptr;
+  if (!host && hipHostMalloc((void**)&host, 2 * sizeof(uint32_t)) != hipSuccess) {
+    host = nullptr;
     return fail(RQSID_E_LAUNCH, "seg_auction: pinned readback buffer");
+  }
   int rc = RQSID_OK;
+  if (hipMemsetAsync(a.live_count, 0, 8, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   hipLaunchKernelGGL(sa_seg_init_kernel, dim3(gs), dim3(256), 0, st, a, active);
   hipLaunchKernelGGL(sa_multi_index_kernel, dim3(1), dim3(1024), 0, st, a);
   if ((rc = check_launch("seg_auction_init")) ||
       hipMemcpyAsync(host, a.live_count, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess) {
-    (void)hipHostFree(host);
+      hipStreamSynchronize(st) != hipSuccess)
     return rc ? rc : fail(RQSID_E_LAUNCH, "seg_auction: init readback");
-  }
-  if ((int32_t)host[1] != n_multi) {
-    (void)hipHostFree(host);
+  if ((int32_t)host[1] != n_multi)
     return fail(RQSID_E_ARG, "seg_auction: %u segments span more than one chunk, n_multi = %d", host[1], n_multi);
-  }
-  if (total_chunks == 0) {
-    (void)hipHostFree(host);
-    return RQSID_OK;
+  if (total_chunks == 0) return RQSID_OK;
+  if (host[0] == 0) {
+    // no segment bids (all inactive, empty or N_s < K): only the argmin fallback runs, no rounds
+    hipLaunchKernelGGL(sa_fallback_kernel, dim3((unsigned)total_chunks), dim3(256), 0, st, a, out_assign);
+    return check_launch("seg_auction_fallback");
   }
   const bool any_single = n_multi < n_seg;
   const size_t mk = (size_t)n_multi * n_workers;
   if (n_multi > 0 && (hipMemsetAsync(a.hist, 0, mk * 256 * 4, st) != hipSuccess ||
                       hipMemsetAsync(a.above, 0, mk * kAbovePad * 4, st) != hipSuccess ||
-                      hipMemsetAsync(a.miss, 1, mk, st) != hipSuccess)) {
-    (void)hipHostFree(host);
+                      hipMemsetAsync(a.miss, 1, mk, st) != hipSuccess))
     return fail(RQSID_E_LAUNCH, "seg_auction: memset");
-  }
   hipLaunchKernelGGL(sa_job_init_kernel, dim3(grid_cap(cdiv(n_jobs, 256), 8192)), dim3(256), 0, st, a, n_jobs);
   const dim3 gcw((unsigned)total_chunks, (unsigned)cdiv(n_workers, kKG));
   const dim3 gc((unsigned)total_chunks);
@@ -873,10 +875,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   hipLaunchKernelGGL(sa_fallback_kernel, gc, dim3(256), 0, st, a, out_assign);
   hipLaunchKernelGGL(sa_minmax_kernel, gcw, dim3(256), 0, st, a);
   hipLaunchKernelGGL(sa_eps_kernel, dim3(gs), dim3(256), 0, st, a);
-  if ((rc = check_launch("seg_auction_init"))) {
-    (void)hipHostFree(host);
-    return rc;
-  }
+  if ((rc = check_launch("seg_auction_init"))) return rc;
   // Rounds run in blocks of kPoll: the live count is read back after each block (rounds of finished
   // segments are no-ops, so stopping late only costs empty launches) and only a block's last round counts,
   // into a counter zeroed after each read.  The round number lives on the device, so one captured block
@@ -946,7 +945,6 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
       rc = fail(RQSID_E_LAUNCH, "seg_auction: %u segments still bidding after %d rounds", host[0], max_rounds);
   }
   if (exec) (void)hipGraphExecDestroy(exec);
-  (void)hipHostFree(host);
   return rc;
 }
 

@@ -33,7 +33,7 @@ import numpy as np
 import torch
 
 from . import ops
-from .balancekmeans import KMeans, _device, batched_fit, init_indices
+from .balancekmeans import KMeans, _device, fit_segments, init_indices
 
 logger = logging.getLogger(__name__)
 
@@ -248,9 +248,9 @@ class HierarchicalRQKMeans:
         self.match_matrices: List[np.ndarray] = []
         self.result_cluster_ids: List[torch.Tensor] = []
         # Sub-K-Means of the middle layer and of the last-layer match matrix: True runs them in lockstep
-        # (balancekmeans.batched_fit: one segmented auction per iteration for all parents / groups);
-        # False runs them one after another as the reference does.  Both draw the numpy RNG in the
-        # reference's segment order; see batched_fit for the one schedule difference (early convergence).
+        # (balancekmeans.fit_segments: one segmented auction per iteration for all parents / groups);
+        # False runs them one after another as the reference does.  Both consume the numpy and torch
+        # random numbers exactly as the reference's loop does.
         self.batched_sub_fits = True
 
     @staticmethod
@@ -381,20 +381,13 @@ class HierarchicalRQKMeans:
         return centers, raw % cur_need, residual
 
     def _batched_middle_fits(self, X, order, off, cur_need, layer, target):
-        """The per-parent balanced fit_by_min_loss runs of :703-725 in lockstep.  Draws, in parent order,
-        each parent's start and every re-initialisation its iteration budget allows (the reference draws a
-        re-initialisation only while the fit has not converged)."""
+        """The per-parent balanced fit_by_min_loss runs of :703-725 in lockstep, drawing numpy and torch
+        random numbers exactly as the one-after-another loop does (balancekmeans.fit_segments)."""
         cfg = self.config
         sizes = np.diff(off).astype(np.int64)
-        limits, inits = [], []
-        for i, n_i in enumerate(sizes):
-            it = adaptive_iter_limit(int(n_i), cur_need, layer, cfg.iter_limit, is_sub_cluster=True)
-            limits.append(it)
-            inits.append([init_indices(int(n_i), cur_need) for _ in range(1 + max(0, (it - 1) // 10))])
-        layout = ops.SegmentLayout(sizes, self.device)
-        xs = X[order].contiguous()
-        centers, _ = batched_fit(xs, layout, cur_need, limits, inits, target_nodes_num=target,
-                                 half=cur_need >= 512)
+        limits = [adaptive_iter_limit(int(n_i), cur_need, layer, cfg.iter_limit, is_sub_cluster=True) for n_i in sizes]
+        centers, _ = fit_segments(X[order].contiguous(), sizes, cur_need, limits, target_nodes_num=target,
+                                  half=cur_need >= 512)
         return centers.contiguous()
 
     def _reassign_clusters_middle_layer_with_residuals(self, X, kmeans_centers, prev_cluster_ids, layer):
@@ -555,9 +548,8 @@ class HierarchicalRQKMeans:
                 centers[g] = sc[i * need:(i + 1) * need]
         if big:
             bsz = sizes[big]
-            layout = ops.SegmentLayout(bsz, self.device)
             limits = [adaptive_iter_limit(int(n), need, layer, base_iter_limit=20) for n in bsz]
-            bc, _ = batched_fit(X[order[rows_of(big)]].contiguous(), layout, need, limits, big_inits, half=False)
+            bc, _ = fit_segments(X[order[rows_of(big)]].contiguous(), bsz, need, limits, big_inits, half=False)
             for i, g in enumerate(big):
                 centers[g] = bc[i * need:(i + 1) * need]
         full = sorted(centers)

@@ -22,7 +22,7 @@ import torch
 
 from . import io as rq_io
 from . import ops
-from .balancekmeans import KMeans, _device, batched_fit, init_indices
+from .balancekmeans import KMeans, _device, fit_segments, init_indices
 from .hierarchical_rq_kmeans import HierarchicalRQKMeansConfig, group_rows, masked_assign, random_fill
 
 logger = logging.getLogger(__name__)
@@ -90,8 +90,8 @@ class SimplifiedHierarchicalRQ:
         if fits:
             fsz = sizes[fits]
             rows = torch.from_numpy(np.concatenate([np.arange(off[i], off[i + 1]) for i in fits])).to(self.device)
-            c, _ = batched_fit(data[order[rows]].contiguous(), ops.SegmentLayout(fsz, self.device), n_need,
-                               [self.config.iter_limit] * len(fits), inits, half=use_half)
+            c, _ = fit_segments(data[order[rows]].contiguous(), fsz, n_need, [self.config.iter_limit] * len(fits),
+                                inits, half=use_half)
             sel = torch.cat([torch.arange(i * n_need, (i + 1) * n_need) for i in fits]).to(self.device)
             out[sel] = c
         return out.contiguous()
@@ -231,8 +231,7 @@ class SimplifiedHierarchicalRQ:
                 fits.append(g)
                 inits.append([init_indices(n_g, n_need)])
         if fits:
-            c, _ = batched_fit(data[order[rows_of(fits)]].contiguous(), ops.SegmentLayout(sizes[fits], self.device),
-                               n_need, [20] * len(fits), inits)
+            c, _ = fit_segments(data[order[rows_of(fits)]].contiguous(), sizes[fits], n_need, [20] * len(fits), inits)
             for i, g in enumerate(fits):
                 centers[g] = c[i * n_need:(i + 1) * n_need]
         full = sorted(centers)

@@ -98,7 +98,11 @@ int32_t rqsid_assign_tile_rows(void);
  * screen_terms: 1 = vh.ch only; 3 = vh.ch + vl.ch + vh.cl (both operands' fp16 rounding
  * residuals, a ~5x tighter bound for 3x the MFMA work; segments of <= 128 candidates only, wider
  * ones use 1); 0 = automatic (3 for residual levels with <= 128 candidates per segment).  The result
- * never depends on it, only the speed. */
+ * never depends on it, only the speed.
+ *
+ * Errors: RQSID_E_ARG / RQSID_E_WORKSPACE before any launch; RQSID_E_LAUNCH for a HIP launch failure
+ * or, on the opt-in centre-resident screen (RQSID_SCREEN_VARIANT=6), when a wave's capped role wait
+ * gave up (device error word read back after the call; the IDs it left are not returned as valid). */
 int64_t rqsid_assign_workspace_bytes(int64_t n_rows);
 int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row_index,
                  int32_t n_segments, const int32_t* seg_row_off, const int32_t* seg_tile_off,

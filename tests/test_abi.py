@@ -46,7 +46,7 @@ def test_host_only_queries_need_no_gpu():
 
 def test_argument_errors_map_to_value_error():
     lib = _lib.load()
-    rc = lib.rqsid_prepare_centers(None, 4, 48, None, None, None, None)  # dim not a multiple of 32
+    rc = lib.rqsid_prepare_centers(None, 4, 48, None, None, None)  # dim not a multiple of 32
     assert rc == -1
     assert "prepare_centers" in lib.rqsid_last_error().decode()
     with pytest.raises(ValueError):

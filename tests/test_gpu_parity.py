@@ -458,3 +458,20 @@ def test_integration_md_binding_runs():
     c = synth.small_mixture(128, d=512, m=50, seed=6)
     got = ns["nearest_center"](torch.from_numpy(x), torch.from_numpy(c)).numpy()
     assert (got == exact_ids(x, c)).all()
+
+
+def test_resident_spin_cap_fails_loudly():
+    """a capped role wait of the centre-resident screen must not return wrong IDs
+    silently.  RQSID_TEST_FORCE_SPIN_CAP gives the screen's final wait a zero cap (every other wait
+    runs normally, so the forced path reads nothing out of order): the device error word is set and
+    rqsid_assign fails with RQSID_E_LAUNCH -> RuntimeError.  Without it the same call succeeds."""
+    rng = np.random.default_rng(3)
+    c = rng.standard_normal((200, 512)).astype(np.float32)
+    x = (c[rng.integers(0, 200, 30000)] + 0.3 * rng.standard_normal((30000, 512))).astype(np.float32)
+    pc = ops.prepare_centers(gpu(c))
+    with pytest.raises(RuntimeError, match="spin cap"):
+        _with_env({"RQSID_SCREEN_VARIANT": 6, "RQSID_TEST_FORCE_SPIN_CAP": 1}, lambda: ops.nearest(gpu(x), pc))
+    got = _with_env({"RQSID_SCREEN_VARIANT": 6, "RQSID_TEST_FORCE_SPIN_CAP": 0},
+                    lambda: ops.nearest(gpu(x), pc).cpu().numpy())
+    sel = np.arange(0, 30000, 29)
+    assert (got[sel] == exact_ids(x[sel], c)).all()
