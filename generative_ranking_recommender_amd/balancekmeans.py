@@ -25,6 +25,14 @@ from . import ops
 
 logger = logging.getLogger(__name__)
 
+# Step tracer for every K-Means fit of this module (tests certify each iteration against the oracle):
+# None, or a callable taking one dict per iteration.  KMeans.fit / fit_by_min_loss send
+# {"kind": "fit", "x", "half", "iteration", "centers_in", "scores" ([K][N] fp16 or None), "assign",
+# "centers_out"}; batched_fit sends {"kind": "batched", "x" (segment-ordered rows), "half", "iteration",
+# "active" (bool [S]), "off" (segment row offsets), "centers_in", "scores" (flat per-segment [K][N_s]
+# blocks or None), "assign" (local ids), "centers_out"}.
+TRACE = None
+
 
 def _device(device) -> torch.device:
     if device is None or (isinstance(device, torch.device) and device.type == "cpu") or device == "cpu":
@@ -94,6 +102,7 @@ class KMeans:
         self.device = _device(device)
         self.balanced = balanced
         self.last_auction_rounds = []
+        self.trace = TRACE  # per-iteration step tracer (see TRACE)
 
     # --- persistence (npz instead of the reference's pickle, :230-239) --------------------------
     @classmethod
@@ -122,11 +131,21 @@ class KMeans:
             raise NotImplementedError(f"distance={distance!r}: only 'euclidean' is on the semantic-ID path")
 
     def _assign(self, X: torch.Tensor, half: bool) -> torch.Tensor:
+        self._scores, self._x, self._half = None, X, half
         if self.balanced:
-            a, rounds = ops.auction(ops.auction_scores(X, self.cluster_centers, half=half))
+            w = ops.auction_scores(X, self.cluster_centers, half=half)
+            a, rounds = ops.auction(w)
             self.last_auction_rounds.append(rounds)
+            if self.trace is not None:
+                self._scores = w
             return a
         return ops.nearest(X, ops.prepare_centers(self.cluster_centers))
+
+    def _emit(self, iteration: int, prev: torch.Tensor, a: torch.Tensor) -> None:
+        if self.trace is not None:
+            self.trace({"kind": "fit", "x": self._x, "half": self._half, "iteration": iteration,
+                        "centers_in": prev.clone(), "scores": self._scores,
+                        "assign": a.clone(), "centers_out": self.cluster_centers.clone()})
 
     def _update(self, X: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
         """:314-324 — per-cluster means; an empty cluster takes X[torch.randint(len(X), (1,))] (CPU RNG,
@@ -159,6 +178,7 @@ class KMeans:
                 self.cluster_centers = self.initialize(X)
             a = self._assign(X, half)
             prev = self._update(X, a)
+            self._emit(iteration, prev, a)
             counts = torch.bincount(ops.nearest(X, ops.prepare_centers(self.cluster_centers)).long(),
                                     minlength=self.n_clusters)
             over = counts - target_nodes_num
@@ -188,6 +208,7 @@ class KMeans:
         while True:
             a = self._assign(X, half)
             prev = self._update(X, a)
+            self._emit(iteration, prev, a)
             center_shift = self._shift(self.cluster_centers, prev)
             iteration += 1
             if center_shift ** 2 < tol:
@@ -278,10 +299,10 @@ def batched_fit(X: torch.Tensor, layout: "ops.SegmentLayout", n_clusters: int, i
                 centers[rows_of[torch.from_numpy(re).to(dev)].reshape(-1)] = gather(
                     [inits[s][iteration[s] // 10] for s in re], re).float()
         act_t = torch.from_numpy(active.astype(np.uint8)).to(dev)
+        w = None
         if balanced:
             w = ops.seg_auction_scores(X, centers, K, layout, half=half)
             a, _ = ops.seg_auction(w, K, layout, act_t, out=last)
-            del w
         else:
             a = ops.assign(X, ops.prepare_centers(centers), buckets, cand)[0]
             keep = ~act_t.bool()[seg_row]
@@ -298,6 +319,11 @@ def batched_fit(X: torch.Tensor, layout: "ops.SegmentLayout", n_clusters: int, i
         frozen = torch.from_numpy(~active).to(dev)
         new[frozen.repeat_interleave(K)] = prev[frozen.repeat_interleave(K)]
         centers = new.contiguous()
+        if TRACE is not None:
+            TRACE({"kind": "batched", "x": X, "half": half, "iteration": iteration.copy(), "active": active.copy(),
+                   "off": off.copy(),
+                   "centers_in": prev.clone(), "scores": w, "assign": a.clone(), "centers_out": centers.clone()})
+        del w
         shift = torch.sqrt(torch.sum((centers - prev) ** 2, dim=1)).view(S, K).sum(1).cpu().numpy()
         if min_loss_mode:
             glob = ops.assign(X, ops.prepare_centers(centers), buckets, cand)[1]

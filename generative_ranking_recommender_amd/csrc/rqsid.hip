@@ -318,8 +318,10 @@ __global__ __launch_bounds__(256) void match_list_kernel(const uint8_t* __restri
 constexpr int kPdTile = 64;
 // MODE 0: out[n][k] = fp32 distance (torch.cdist, pairwise_distance_full balancekmeans/__init__.py:576-603)
 // MODE 1: out16[k][n] = fp16(-distance): the auction's worker-major score matrix (auction_lap_half(-D), :29-43)
-// MODE 2: as 1 from fp16-rounded operands with the distance rounded to fp16 and clamped at 1e-5
-//         (pairwise_distance_half, :536-574)
+// MODE 2: pairwise_distance_half (:536-574) with torch's fp16 arithmetic (ATen _euclidean_dist on half
+//         tensors): operands rounded to fp16, |x|^2 = fp16(sum fp16(x_i^2)), d^2 = fp16(-2 x.c + |x|^2 +
+//         |c|^2) (exact fp16 products, fp32 accumulation), d = fp16(sqrt(max(d^2, 0))), clamp(min=1e-5);
+//         then negated into the worker-major score matrix (oracle.cdist_half)
 //
 // SEG (modes 1/2 only): segment s owns rows seg_off[s]..seg_off[s+1] and centres s*k .. s*k+k-1; its
 // scores go to out16 + k*seg_off[s] as a [k][n_s] worker-major block (the segmented auction's layout).
@@ -380,13 +382,25 @@ __global__ __launch_bounds__(256) void pairwise_distance_kernel(const float* __r
       for (int j = 0; j < 4; ++j) bb[j] = cs[tx + 16 * j][dd];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        xq[i] = fmaf(a[i], a[i], xq[i]);
-        cq[i] = fmaf(bb[i], bb[i], cq[i]);
+        if (MODE == 2) {  // x.pow(2) is an fp16 tensor: every square rounded to fp16 before the sum
+          xq[i] += (float)(_Float16)(a[i] * a[i]);
+          cq[i] += (float)(_Float16)(bb[i] * bb[i]);
+        } else {
+          xq[i] = fmaf(a[i], a[i], xq[i]);
+          cq[i] = fmaf(bb[i], bb[i], cq[i]);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], bb[j], acc[i][j]);
       }
     }
     __syncthreads();
+  }
+  if (MODE == 2) {  // the norms are fp16 tensors
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      xq[i] = (float)(_Float16)xq[i];
+      cq[i] = (float)(_Float16)cq[i];
+    }
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -396,7 +410,8 @@ __global__ __launch_bounds__(256) void pairwise_distance_kernel(const float* __r
     for (int j = 0; j < 4; ++j) {
       const int cc = c0 + tx + 16 * j;
       if (cc >= k) continue;
-      const float d2 = (-2.f * acc[i][j] + xq[i]) + cq[j];
+      const float d2 = MODE == 2 ? (float)(_Float16)((-2.f * acc[i][j] + xq[i]) + cq[j])
+                                 : (-2.f * acc[i][j] + xq[i]) + cq[j];
       const float d = sqrtf(fmaxf(d2, 0.f));
       if (MODE == 0) {
         out[rr * k + cc] = d;

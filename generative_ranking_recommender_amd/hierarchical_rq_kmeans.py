@@ -239,8 +239,9 @@ class HierarchicalRQKMeans:
     """hierarchical_rq_kmeans.py:187-1409."""
 
     def __init__(self, config: HierarchicalRQKMeansConfig, checkpoint_dir: Optional[str] = None,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, group=None):
         self.config = config
+        self.group = group  # torch.distributed group: row-sharded training / encode (SURVEY.md §8e)
         self.device = _device(device)
         self.checkpoint_manager = CheckpointManager(checkpoint_dir) if checkpoint_dir else None
         self.is_trained = False

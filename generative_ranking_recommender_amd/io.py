@@ -8,8 +8,9 @@
   include/rqsid_io.h); the Python-csv restatement it is checked against is ``oracle/csv_oracle.py``.
 * ``write_semantic_ids`` — one ``json.dumps({"song_id": ..., "semantic_ids": [...]})`` line per song
   (simplified :368-385, train_semantic_ids.py:239-264), byte-identical to the reference.
-* ``semantic_id_statistics`` / ``training_config`` — the side files training_statistics.json and
-  training_config.json of train_semantic_ids.py:266-333.
+* ``semantic_id_statistics`` / ``training_config`` (+ ``json_bytes``) — the side files
+  training_statistics.json and training_config.json of train_semantic_ids.py:266-365, byte-identical
+  (``generative_ranking_recommender_amd.train_semantic_ids.SemanticIDTrainer`` writes them).
 """
 from __future__ import annotations
 
@@ -117,6 +118,25 @@ def semantic_id_statistics(semantic_ids: Dict[str, List[int]], need_clusters: Se
     return stats
 
 
+def training_config(config, use_test_config: bool) -> Dict:
+    """train_semantic_ids.py:266-288 _save_config: the side file training_config.json (same keys, same
+    order)."""
+    return {
+        "layer_clusters": config.layer_clusters,
+        "need_clusters": config.need_clusters,
+        "embedding_dim": config.embedding_dim,
+        "group_dims": config.group_dims,
+        "hierarchical_weights": config.hierarchical_weights,
+        "iter_limit": config.iter_limit,
+        "use_test_config": use_test_config,
+    }
+
+
+def json_bytes(obj) -> bytes:
+    """The reference's side-file encoding: json.dump(obj, f, indent=2, ensure_ascii=False) in UTF-8."""
+    return json.dumps(obj, indent=2, ensure_ascii=False).encode("utf-8")
+
+
 def write_json(path: str, obj) -> None:
-    with open(path, "w", encoding="utf-8") as f:
-        json.dump(obj, f, indent=2, ensure_ascii=False)
+    with open(path, "wb") as f:
+        f.write(json_bytes(obj))

@@ -38,6 +38,86 @@ def cdist_f32(x: np.ndarray, c: np.ndarray) -> np.ndarray:
     return np.sqrt(np.maximum(d2, F32(0.0)), dtype=F32)
 
 
+def cdist_half(x: np.ndarray, c: np.ndarray) -> np.ndarray:
+    """pairwise_distance_half (balancekmeans/__init__.py:536-574): ``torch.cdist`` of the fp16-rounded
+    operands, clamped at 1e-5, with torch's fp16 arithmetic (ATen ``_euclidean_dist`` on half tensors,
+    as measured against torch 2.10 CPU in tests/test_oracle_golden.py):
+      |x|^2 = fp16(sum_i fp16(x_i^2))                   (x.pow(2) is an fp16 tensor; fp32 accumulation)
+      d^2   = fp16([-2x, |x|^2, 1] . [c, 1, |c|^2])      (fp16 x fp16 products exact; fp32 accumulation)
+      d     = fp16(sqrt(max(d^2, 0)));  clamp(min=1e-5)  (the fp16 of 1e-5 is 168 * 2^-24)
+    The fp32 accumulation order inside torch's kernels is not reproduced: ``half_dist_interval`` bounds
+    what any order can give."""
+    f16 = np.float16
+    xh = np.asarray(x, F32).astype(f16).astype(F32)
+    ch = np.asarray(c, F32).astype(f16).astype(F32)
+    xn = (xh * xh).astype(f16).astype(F32).sum(1, dtype=F32).astype(f16).astype(F32)
+    cn = (ch * ch).astype(f16).astype(F32).sum(1, dtype=F32).astype(f16).astype(F32)
+    d2 = (((F32(-2.0) * xh) @ ch.T + xn[:, None]).astype(F32) + cn[None, :]).astype(F32).astype(f16)
+    d = np.sqrt(np.maximum(d2.astype(F32), F32(0.0))).astype(f16)
+    return np.maximum(d, f16(1e-5))
+
+
+def _fp32_sum_bound(n_terms: int) -> float:
+    """First-order bound on the relative (to sum |t|) error of an fp32 sum of n terms in any order."""
+    return (n_terms - 1) * 2.0 ** -24 * 1.0001
+
+
+def half_dist_interval(x: np.ndarray, c: np.ndarray):
+    """[lo, hi] (fp16 values as float64) of every result ``pairwise_distance_half`` can give under ANY
+    fp32 accumulation order of its two sums (the norms and the augmented product): the arbiter for a
+    mismatch between two correct implementations (the reference's torch kernels and the HIP kernel)."""
+    f16 = np.float16
+    xh = np.asarray(x, F32).astype(f16).astype(np.float64)
+    ch = np.asarray(c, F32).astype(f16).astype(np.float64)
+    d = xh.shape[1]
+
+    def norm_range(v):
+        sq = (v * v).astype(f16).astype(np.float64)
+        t = sq.sum(1)
+        e = _fp32_sum_bound(d) * t
+        return (t - e).astype(f16).astype(np.float64), (t + e).astype(f16).astype(np.float64)
+
+    xlo, xhi = norm_range(xh)
+    clo, chi = norm_range(ch)
+    dot = -2.0 * (xh @ ch.T)
+    mag = 2.0 * (np.abs(xh) @ np.abs(ch).T)
+    lo = dot + xlo[:, None] + clo[None, :]
+    hi = dot + xhi[:, None] + chi[None, :]
+    e = _fp32_sum_bound(d + 2) * (mag + xhi[:, None] + chi[None, :])
+    lo, hi = lo - e, hi + e
+
+    def fin(v):
+        v16 = np.maximum(v.astype(f16).astype(F32), F32(0.0))
+        return np.maximum(np.sqrt(v16).astype(f16), f16(1e-5)).astype(np.float64)
+
+    return fin(lo), fin(hi)
+
+
+def full_dist_interval(x: np.ndarray, c: np.ndarray):
+    """[lo, hi] of fp16(cdist_fp32(x, c)) (``auction_lap_half(-pairwise_distance_full)``'s input, :29)
+    over any fp32 summation order of torch.cdist's mm expansion (|x|^2, |c|^2 and the augmented
+    product)."""
+    f16 = np.float16
+    xd = np.asarray(x, F32).astype(np.float64)
+    cd = np.asarray(c, F32).astype(np.float64)
+    d = xd.shape[1]
+    xn = (xd * xd).sum(1)
+    cn = (cd * cd).sum(1)
+    exact = xn[:, None] + cn[None, :] - 2.0 * (xd @ cd.T)
+    e = _fp32_sum_bound(d + 2) * (2.0 * (np.abs(xd) @ np.abs(cd).T) + xn[:, None] + cn[None, :]) * 2.0
+    lo = np.sqrt(np.maximum(exact - e, 0.0)).astype(F32).astype(f16).astype(np.float64)
+    hi = np.sqrt(np.maximum(exact + e, 0.0)).astype(F32).astype(f16).astype(np.float64)
+    return lo, hi
+
+
+def uncertified(got, ref, lo, hi) -> np.ndarray:
+    """Mask of entries where got != ref and one of them lies outside the [lo, hi] interval any
+    summation order can produce (a real arithmetic difference, not an order effect)."""
+    g = np.asarray(got, np.float64)
+    r = np.asarray(ref, np.float64)
+    return (g != r) & ((g < lo) | (g > hi) | (r < lo) | (r > hi))
+
+
 def exact_d2(x: np.ndarray, c: np.ndarray) -> np.ndarray:
     """fp64 squared distances (the arbiter for near ties)."""
     x = x.astype(np.float64)
@@ -270,6 +350,102 @@ def auction_lap_half(job_and_worker_to_score: np.ndarray, tie_rule: str = "torch
         index = high_bidders * num_jobs + jobs_with_bidder
         value.reshape(-1)[index] = w.reshape(-1)[index]
         counter += 1
+
+
+def _auction_select(value: np.ndarray, jpw: int, tie_rule: str) -> np.ndarray:
+    """top_index of ``value.topk(jpw + 1, dim=1)`` (balancekmeans/__init__.py:64-73) under a tie rule."""
+    if tie_rule == "torch":
+        import torch
+        return torch.from_numpy(value).topk(jpw + 1, dim=1)[1].numpy()
+    num_workers, num_jobs = value.shape
+    order = np.lexsort((np.arange(num_jobs)[None, :].repeat(num_workers, 0), -value.astype(F32)), axis=1)
+    return order[:, :jpw + 1]
+
+
+def _auction_max(sub: np.ndarray, tie_rule: str):
+    """``bids[:, jobs_with_bidder].max(dim=0)`` (:104) -> (high_bids, high_bidders)."""
+    if tie_rule == "torch":
+        import torch
+        hb, hbr = torch.from_numpy(np.ascontiguousarray(sub)).max(dim=0)
+        return hb.numpy(), hbr.numpy()
+    hbr = sub.argmax(0)
+    return sub[hbr, np.arange(sub.shape[1])], hbr
+
+
+def auction_tie_certificate(job_and_worker_to_score: np.ndarray) -> dict:
+    """Certify that two implementations of auction_lap_half (:12-140) that differ only in which of
+    several EQUAL values they keep can disagree: the reference's own choice (torch.topk / torch.max on
+    the CPU, ``tie_rule="torch"``) and the lowest-index rule of the HIP kernels (``"stable"``) are run in
+    lockstep on the same fp16 scores.  While the two states are identical, every round's two selections
+    are compared; the first round where they differ is returned with ``tie_born`` = every differing
+    selection is among jobs whose value equals that worker's (jpw+1)-th largest (the topk boundary),
+    or, for the max over bidders, among equal bids.  After that round the trajectories legitimately
+    part.  Returns {"diverged", "round", "step", "tie_born", "torch", "stable"} (the two results; without
+    a divergence both are the lockstep run's)."""
+    s = np.asarray(job_and_worker_to_score, dtype=F32)
+    num_jobs, num_workers = s.shape
+    out = {"diverged": False, "round": -1, "step": None, "tie_born": True}
+    if num_jobs < num_workers:
+        out["torch"] = out["stable"] = auction_lap_half(s)
+        return out
+
+    def parted(**kw):
+        out.update(diverged=True, **kw)
+        out["torch"] = auction_lap_half(s, tie_rule="torch")
+        out["stable"] = auction_lap_half(s, tie_rule="stable")
+        return out
+    s16 = s.astype(np.float16)
+    spread = np.float16(s16.max().astype(F32) - s16.min().astype(F32))
+    eps = max(np.float16(F32(spread) / F32(50.0)), np.float16(1e-4))
+    w = np.ascontiguousarray(s16.T)
+    jpw = num_jobs // num_workers
+    value = w.copy()
+    cost = np.zeros(num_jobs, dtype=np.float16)
+    counter, index, jobs_without_bidder = 0, None, None
+    while True:
+        ti = _auction_select(value, jpw, "torch")
+        si = _auction_select(value, jpw, "stable")
+        for wk in range(num_workers):
+            bt, bs = set(ti[wk, :-1].tolist()), set(si[wk, :-1].tolist())
+            if bt != bs or ti[wk, -1] != si[wk, -1]:
+                thr = value[wk, si[wk, -1]]
+                diff = (bt ^ bs) | {int(ti[wk, -1]), int(si[wk, -1])}
+                return parted(round=counter, step="topk",
+                              tie_born=bool(value[wk, ti[wk, -1]] == thr and all(value[wk, j] == thr for j in diff)))
+        top_values = np.take_along_axis(value, ti, 1)
+        inc = ((top_values[:, :-1].astype(F32) - top_values[:, -1:].astype(F32)).astype(np.float16).astype(F32)
+               + F32(eps)).astype(np.float16)
+        bids = np.zeros((num_workers, num_jobs), dtype=np.float16)
+        np.put_along_axis(bids, ti[:, :-1], inc, 1)
+        if counter < 100 and index is not None:
+            bids.reshape(-1)[index] = eps
+        if counter > 1000:
+            bids.reshape(-1)[jobs_without_bidder] = eps
+        jobs_with_bidder = np.nonzero((bids > 0).any(0))[0]
+        jobs_without_bidder = np.nonzero((bids == 0).all(0))[0]
+        sub = bids[:, jobs_with_bidder]
+        hb, hbr = _auction_max(sub, "torch")
+        hb_s, hbr_s = _auction_max(sub, "stable")
+        if not np.array_equal(hbr, hbr_s):
+            k = np.nonzero(hbr != hbr_s)[0]
+            return parted(round=counter, step="max", tie_born=bool((sub[hbr[k], k] == sub[hbr_s[k], k]).all()))
+        if len(hbr) == num_jobs:
+            out["torch"] = out["stable"] = hbr.astype(np.int64)
+            return out
+        cost[jobs_with_bidder] = (cost[jobs_with_bidder].astype(F32) + hb.astype(F32)).astype(np.float16)
+        value = (w.astype(F32) - cost[None, :].astype(F32)).astype(np.float16)
+        index = hbr * num_jobs + jobs_with_bidder
+        value.reshape(-1)[index] = w.reshape(-1)[index]
+        counter += 1
+
+
+def assignment_quality(job_and_worker_to_score: np.ndarray, assign: np.ndarray) -> dict:
+    """What a balanced assignment optimises and promises: the total fp32 score of the chosen pairs and
+    the per-worker job counts (the balance histogram)."""
+    s = np.asarray(job_and_worker_to_score, dtype=np.float64)
+    a = np.asarray(assign, dtype=np.int64)
+    return {"score": float(s[np.arange(len(a)), a].sum()),
+            "counts": np.bincount(a, minlength=s.shape[1])}
 
 
 def auction_lap_full(job_and_worker_to_score: np.ndarray, tie_rule: str = "torch") -> np.ndarray:

@@ -60,3 +60,18 @@ def prod_encode_inputs(g):
     assert synth.codebooks_sha(cb) == str(g["cb_sha"])
     x = checked(synth.mixture_rows(0, 2000), g["x_sha"])
     return x, cb
+
+
+def half_inputs(g):
+    """tests/golden/make_golden.py half_inputs (pairwise_distance_half fixture)."""
+    x = synth.small_mixture(640, m=32, seed=41)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    c = synth.small_mixture(520, m=32, seed=42)
+    c /= np.linalg.norm(c, axis=1, keepdims=True)
+    c[:5] = x[:5]
+    x2 = synth.small_mixture(300, m=16, seed=43) * np.float32(3.0)
+    c2 = synth.small_mixture(600, m=16, seed=44) * np.float32(3.0)
+    x, c, x2, c2 = (a.astype(np.float32) for a in (x, c, x2, c2))
+    for a, key in ((x, "x_sha"), (c, "c_sha"), (x2, "x2_sha"), (c2, "c2_sha")):
+        checked(a, g[key])
+    return x, c, x2, c2

@@ -159,6 +159,37 @@ def g_auction_full():
     save("auction_full", **res)
 
 
+# --- G-half: pairwise_distance_half (fp16 cdist + clamp at 1e-5, the K >= 512 auction input) ---
+def half_inputs():
+    """normalised-residual-like rows (unit norm) and 520 centres, five of them equal to rows (zero
+    distance -> the clamp at 1e-5); a second, unnormalised set at another scale"""
+    x = synth.small_mixture(640, m=32, seed=41)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    c = synth.small_mixture(520, m=32, seed=42)
+    c /= np.linalg.norm(c, axis=1, keepdims=True)
+    c[:5] = x[:5]
+    x2 = synth.small_mixture(300, m=16, seed=43) * np.float32(3.0)
+    c2 = synth.small_mixture(600, m=16, seed=44) * np.float32(3.0)
+    return x.astype(np.float32), c.astype(np.float32), x2.astype(np.float32), c2.astype(np.float32)
+
+
+def g_dist_half():
+    """The reference's CPU branch of pairwise_distance_half computes ``int(free_mem / ...)`` with
+    ``free_mem = float('inf')`` (:552-553), which raises OverflowError: the function only runs on CUDA
+    as written.  Like the batch-size patch above, the harness makes that batch size finite: the module's
+    global name ``float`` is shadowed so ``float('inf')`` gives 1e18 (only the chunking of the loop at
+    :563-569 depends on it; the arithmetic is the reference's own torch.cdist + clamp on fp16 tensors)."""
+    ref_bk.float = lambda v: 1e18 if v == "inf" else float(v)
+    x, c, x2, c2 = half_inputs()
+    d = ref_bk.pairwise_distance_half(torch.from_numpy(x), torch.from_numpy(c))
+    d2 = ref_bk.pairwise_distance_half(torch.from_numpy(x2), torch.from_numpy(c2))
+    assert d.dtype == torch.float16
+    del ref_bk.float
+    save("dist_half", x_sha=np.array(synth.sha256(x)), c_sha=np.array(synth.sha256(c)),
+         x2_sha=np.array(synth.sha256(x2)), c2_sha=np.array(synth.sha256(c2)),
+         d=d.numpy().view(np.uint16), d2=d2.numpy().view(np.uint16))
+
+
 # --- G6: fit_by_min_loss / fit (balanced) trajectories ----------------------
 def g_fit():
     X = synth.small_mixture(512, m=16, seed=23)
@@ -240,6 +271,35 @@ def g_hierarchical():
          new_fix_keyerror=np.array(new_fix_err))
 
 
+# --- G-trainer: the reference's driver SemanticIDTrainer (train_semantic_ids.py:35-365) end to end ---
+def g_trainer():
+    """train_semantic_ids.SemanticIDTrainer(config, use_test_config=True).train(resume=False) on a small
+    CSV: the side files training_config.json / training_statistics.json and the jsonl, as bytes."""
+    from src.semantic_id_generator import train_semantic_ids as ref_t
+    X = synth.small_mixture(2048, m=64, seed=21)
+    sids = [f"s{i:05d}" for i in range(len(X))]
+    with tempfile.TemporaryDirectory() as td:
+        csv_path = os.path.join(td, "vec.csv")
+        write_csv(csv_path, sids, X)
+        cfg = types.SimpleNamespace(
+            output_dir=os.path.join(td, "outputs"), model_dir=os.path.join(td, "models"),
+            h_rqkmeans_test=ref_h.HierarchicalRQKMeansConfig(**SMALL_CFG), h_rqkmeans=None,
+            data=types.SimpleNamespace(song_vectors_file=csv_path,
+                                       semantic_ids_file=os.path.join(td, "outputs", "semantic_id",
+                                                                      "song_semantic_ids.jsonl")))
+        seed_all(42)
+        trainer = ref_t.SemanticIDTrainer(cfg, use_test_config=True)
+        res = trainer.train(resume=False)
+        out = Path(td) / "outputs" / "semantic_id"
+        cfg_bytes = (out / "training_config.json").read_bytes()
+        stats_bytes = (out / "training_statistics.json").read_bytes()
+        jsonl = (out / "song_semantic_ids.jsonl").read_bytes()
+    ids = np.array([res["semantic_ids"][s] for s in sids], dtype=np.int64)
+    save("trainer", x_sha=np.array(synth.sha256(X)), ids=ids,
+         config_json=np.frombuffer(cfg_bytes, dtype=np.uint8), stats_json=np.frombuffer(stats_bytes, dtype=np.uint8),
+         jsonl_sha=np.array(synth.sha256(np.frombuffer(jsonl, dtype=np.uint8))))
+
+
 # --- G-encode: predict at PROD codebook shapes [128,1280,1280]/[128,128,256] --
 def g_encode_prod():
     cb = synth.encode_codebooks(seed=99)
@@ -294,6 +354,6 @@ def g_csv():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["assign", "residual", "update", "auction", "fit", "simplified",
-                             "hierarchical", "encode_prod", "csv"]
+                             "hierarchical", "encode_prod", "csv", "dist_half", "trainer"]
     for w in which:
         globals()[f"g_{w}"]()

@@ -151,3 +151,65 @@ def test_prod_shape_encode_matches_reference(golden):
         ids = O.encode(x, cents, need, cb["match"], **kw)
         bad = np.nonzero((ids != g[key]).any(1))[0]
         assert len(bad) == 0, f"{key}: {len(bad)} rows differ"
+
+
+def _half_case(g, which):
+    from tests import _data
+    x, c, x2, c2 = _data.half_inputs(g)
+    return (x, c, g["d"]) if which == 1 else (x2, c2, g["d2"])
+
+
+@pytest.mark.parametrize("which", [1, 2])
+def test_cdist_half_matches_reference(golden, which):
+    """pairwise_distance_half (balancekmeans/__init__.py:536-574; the input of every auction at K >= 512):
+    the oracle's restatement of torch's fp16 cdist vs the reference's own output.  A mismatch is allowed
+    only where the fp32 accumulation order (torch's kernels vs numpy's) can legitimately change the fp16
+    result: both values inside O.half_dist_interval."""
+    x, c, d_ref = _half_case(golden("dist_half"), which)
+    ref = d_ref.view(np.float16)
+    got = O.cdist_half(x, c)
+    lo, hi = O.half_dist_interval(x, c)
+    assert not O.uncertified(got, ref, lo, hi).any()
+    assert ((ref >= lo) & (ref <= hi)).all()
+    assert (got != ref).mean() < 1e-3
+    if which == 1:
+        # equal operands: fp16 cancellation leaves d^2 = 0 (-> the clamp at 1e-5) or a few fp16 ulps
+        diag = ref[np.arange(5), np.arange(5)]
+        assert (diag == np.float16(1e-5)).any() and (diag < np.float16(1e-2)).all()
+
+
+def test_trainer_side_files_match_reference(golden):
+    """train_semantic_ids.py:239-365: training_config.json, training_statistics.json and the jsonl written
+    by the reference's SemanticIDTrainer, byte for byte, from the same IDs / config."""
+    from generative_ranking_recommender_amd import io as rq_io, synth
+    from generative_ranking_recommender_amd.hierarchical_rq_kmeans import HierarchicalRQKMeansConfig
+    g = golden("trainer")
+    cfg = HierarchicalRQKMeansConfig(**_data.SMALL_CFG)
+    assert rq_io.json_bytes(rq_io.training_config(cfg, True)) == bytes(g["config_json"])
+    sids = [f"s{i:05d}" for i in range(len(g["ids"]))]
+    semantic = {s: [int(v) for v in row] for s, row in zip(sids, g["ids"])}
+    assert rq_io.json_bytes(rq_io.semantic_id_statistics(semantic, cfg.need_clusters)) == bytes(g["stats_json"])
+    raw = O.jsonl_lines(sids, g["ids"])
+    assert synth.sha256(np.frombuffer(raw, dtype=np.uint8)) == str(g["jsonl_sha"])
+    assert (g["ids"] == golden("hierarchical")["train_ids"]).all()  # the driver trains what G3 trained
+
+
+@pytest.mark.parametrize("reader", ["oracle", "native"])
+def test_csv_loader_matches_reference(golden, tmp_path, reader):
+    """simplified_semantic_id_generator.py:38-76: the reference loader's own output on a file exercising
+    its skip rules (too few fields, non-numeric, wrong dimension, duplicate ids, padded numbers) and the
+    fp16 rule (any layer_clusters > 512), for the CSV restatement and the native reader."""
+    from oracle import csv_oracle
+    from generative_ranking_recommender_amd import io as rq_io
+    g = golden("csv")
+    p = tmp_path / "v.csv"
+    p.write_bytes(bytes(g["text"]))
+    def load(path, dim, lc):
+        out = (csv_oracle.load_song_vectors if reader == "oracle" else rq_io.load_song_vectors)(path, dim, lc)
+        return out[0], out[1]
+    ids, x = load(str(p), 4, [2])
+    assert ids == [str(s) for s in g["sids"]]
+    assert x.dtype == np.float32 and np.array_equal(x, g["emb"])
+    ids_h, x_h = load(str(p), 4, [600])
+    assert str(g["emb_half_dtype"]) == "torch.float16" and x_h.dtype == np.float16
+    assert np.array_equal(x_h.view(np.uint16), g["emb_half"].view(np.uint16))
