@@ -33,7 +33,9 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
 from generative_ranking_recommender_amd import ops, synth  # noqa: E402
-from generative_ranking_recommender_amd.encode import HIERARCHICAL_TRAIN, RQEncoder  # noqa: E402
+from generative_ranking_recommender_amd.encode import HIERARCHICAL_TRAIN  # noqa: E402
+from generative_ranking_recommender_amd.hierarchical_rq_kmeans import (  # noqa: E402
+    HierarchicalRQKMeans, HierarchicalRQKMeansConfig)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA spec
@@ -63,6 +65,9 @@ def parse():
                     help="rows of the balanced (auction) training iterations in 'train_balanced' (0 = skip)")
     ap.add_argument("--train-iters", type=int, default=3,
                     help="Lloyd iterations timed for the 'train' field (0 = skip)")
+    ap.add_argument("--config0", type=int, default=1,
+                    help="1: also run BASELINE configs[0] (100k, single level K=128, simplified path) on the GPU and "
+                         "its CPU restatement on a bounded sample (field 'config0')")
     ap.add_argument("--parity-rows", type=int, default=2048,
                     help="rows of the timed output checked against the exact CPU oracle after the run (0 = skip)")
     a = ap.parse_args()
@@ -194,6 +199,59 @@ def cpu_baseline(cb, rows):
                       f"{dt:.2f} s"}
 
 
+def config0(dev, rows=100_000, cpu_rounds=40):
+    """BASELINE configs[0]: 100k x 512, single level K=128, the simplified path (simplified_semantic_id_
+    generator.py:176-245 with layer_clusters = need = [128]: one balanced fit_by_min_loss with target
+    np.prod([]) = 1.0 (Appendix A item 9), then predict).  GPU: the whole SimplifiedHierarchicalRQ.train
+    on the HIP path (train_rows: rows already loaded).  CPU: the oracle's restatement of one Lloyd
+    iteration of that fit (fp32 cdist + auction_lap_half + update) timed on a bounded sample of
+    ``cpu_rounds`` auction rounds and scaled to the iteration's rounds (1002 here: N % K != 0)."""
+    from generative_ranking_recommender_amd.simplified_semantic_id_generator import SimplifiedHierarchicalRQ
+    from oracle import rq_oracle as O
+    xs = synth.mixture_rows(0, rows)
+    cfg = HierarchicalRQKMeansConfig(layer_clusters=[128], need_clusters=[128], embedding_dim=D)
+    m = SimplifiedHierarchicalRQ(cfg, device=dev)
+    np.random.seed(42)
+    torch.manual_seed(42)
+    sids = [str(i) for i in range(rows)]
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    m.train_rows(sids, torch.from_numpy(xs))
+    torch.cuda.synchronize()
+    gpu_s = time.perf_counter() - t
+    km = m.trained_kmeans_models[0]
+    iters = len(km.last_auction_rounds)
+    ids = np.array([m.semantic_ids[s][0] for s in sids[:4096]])
+    out = {"workload": f"SimplifiedHierarchicalRQ.train, {rows} x {D}, layer_clusters = need_clusters = [128], "
+                       f"iter_limit {cfg.iter_limit} (BASELINE configs[0])",
+           "gpu": {"seconds": round(gpu_s, 2), "iterations": iters,
+                   "auction_rounds": int(np.sum(km.last_auction_rounds)),
+                   "s_per_iteration": round(gpu_s / max(iters, 1), 4),
+                   "ids_in_range": bool((ids >= 0).all() and (ids < 128).all())}}
+    # the CPU restatement of one iteration (the reference's own arithmetic, numpy)
+    rng = np.random.default_rng(0)
+    c = xs[rng.choice(rows, 128, replace=False)]
+    t = time.perf_counter()
+    d = O.cdist_f32(xs, c)
+    t_d = time.perf_counter() - t
+    t_r = O.auction_rounds_torch_cpu(-d, cpu_rounds)
+    a = d.argmin(1)
+    t = time.perf_counter()
+    O.centroid_update(xs, a, c, lambda n: 0)
+    t_u = time.perf_counter() - t
+    rounds = 1002 if rows % 128 else 13
+    cpu_iter = t_d + rounds * t_r + t_u
+    from threadpoolctl import threadpool_info
+    threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    out["cpu_baseline"] = {"value": round(cpu_iter, 2), "unit": "s per balanced Lloyd iteration", "cores": int(threads),
+                           "kind": "port",
+                           "sample": f"oracle/rq_oracle.py: cdist {t_d:.2f} s (numpy) + {cpu_rounds} auction rounds "
+                                     f"at {t_r * 1e3:.1f} ms (torch CPU ops, scaled to {rounds}) + update {t_u:.2f} s; "
+                                     f"{threads} BLAS threads, torch {torch.get_num_threads()} threads"}
+    out["gpu_vs_cpu_per_iteration"] = round(cpu_iter / max(out["gpu"]["s_per_iteration"], 1e-9), 1)
+    return out
+
+
 def train_iterations(x, c0, iters, world, n_global):
     """§8(d)'s training unit: rows x Lloyd iterations at level 0 (K = 128, unbalanced KMeans.fit step,
     balancekmeans/__init__.py:368-465): exact assign (rqsid_assign) + fp64 per-cluster sums and counts
@@ -317,8 +375,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    import torch.distributed as tdist
     if dist:
-        import torch.distributed as tdist
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         tdist.init_process_group("nccl")
@@ -326,8 +384,16 @@ def main():
     torch.cuda.set_device(dev)
 
     cb = codebooks(args.codebooks, dev)
-    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], NEED, match=torch.from_numpy(cb["match"]),
-                    semantics=HIERARCHICAL_TRAIN, device=dev)
+    # the library entry point: a trained HierarchicalRQKMeans (row-sharded over the process group when N > 1)
+    # whose encode_shard is the hot path of predict (training-consistent semantics, IDs stay on the device)
+    model = HierarchicalRQKMeans(HierarchicalRQKMeansConfig(layer_clusters=[NEED[0], N_CAND // 2, N_CAND // 2],
+                                                            need_clusters=list(NEED), embedding_dim=D),
+                                 device=dev, group=tdist.group.WORLD if dist else None)
+    model.cluster_centers_list = [torch.from_numpy(cb[k]).to(dev) for k in ("c0", "c1", "c2")]
+    model.match_matrices = [cb["match"]]
+    model.is_trained = True
+    enc = model._encoder(reference_quirks=False)
+    assert enc.sem == HIERARCHICAL_TRAIN
     n = args.rows
     x = make_rows(n, rank, dev)
     torch.cuda.synchronize()
@@ -361,12 +427,20 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         level["i"] = 0
-        out = enc.encode(x)
+        out = model.encode_shard(x)
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
     encmod.ops.assign, encmod.ops.residual, encmod.ops.bucket = orig_assign, orig_res, orig_bucket
+    gather_ms = None
+    if dist:  # outside the timed region: the int32 IDs of every rank to every rank (the jsonl writer's input)
+        t_g = time.perf_counter()
+        ids_all = model.gather_ids(out)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - t_g) * 1e3
+        assert ids_all.shape[0] == n * world
+        del ids_all
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if dist:
@@ -434,11 +508,14 @@ def main():
                                f"[{NEED[0]},{N_CAND // 2},{N_CAND // 2}] (BASELINE "
                                + ("configs[2]/[3])" if NEED[0] == 128 else "configs[4] encode shapes)"),
                    "rows_per_gpu": n, "dim": D, "need_clusters": NEED, "candidates_last_level": N_CAND,
-                   "parallelism": f"rows sharded x{world}, no collective",
+                   "parallelism": f"rows sharded x{world}, no collective in the step",
+                   "entry_point": "HierarchicalRQKMeans.encode_shard (the per-rank hot path of predict)",
                    "method": "fp16 MFMA screen (LDS-DMA ring) + fp64 re-score (exact argmin)"},
         "roofline": roof,
         "kernels": kern,
     }
+    if gather_ms is not None:
+        line["gather_ids_ms"] = round(gather_ms, 3)
     if args.train_iters > 0:
         t_ms, rps = train_iterations(x, torch.from_numpy(cb["c0"]).to(dev).float(), args.train_iters, world, n * world)
         line["train"] = {"metric": "rows x Lloyd iterations/sec (level 0, K=128: assign + fp64 centroid update"
@@ -454,6 +531,11 @@ def main():
         line["parity"] = check_sample(x, out, cb, args.parity_rows)
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
         line["cpu_baseline"] = cpu_baseline(cb, args.cpu_sample)
+    if rank == 0 and world == 1 and args.config0:
+        try:
+            line["config0"] = config0(dev)
+        except Exception as exc:  # a side measurement must not cost the encode line
+            line["config0"] = {"error": repr(exc)[:300]}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:

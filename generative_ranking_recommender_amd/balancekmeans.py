@@ -350,7 +350,7 @@ def reinit_draws(iter_limit: int) -> int:
 
 
 def fit_segments(X: torch.Tensor, sizes, n_clusters: int, iter_limits, inits=None, target_nodes_num=None,
-                 tol: float = 1e-3, half: bool = False, max_restarts: int = 3):
+                 tol: float = 1e-3, half: bool = False, max_restarts: int = 3, comm=None, owned=None):
     """The reference's one-after-another sub-fits (hierarchical_rq_kmeans.py:703-731, 1010-1019;
     simplified_semantic_id_generator.py:119-133, 275-278) run in lockstep by ``batched_fit``, with the
     reference's random-number consumption restored exactly.
@@ -370,52 +370,79 @@ def fit_segments(X: torch.Tensor, sizes, n_clusters: int, iter_limits, inits=Non
     one segment at a time, which is exact by construction.  Without ``target_nodes_num`` (``fit``) the
     caller draws the starts (``inits[s] = [indices]``) in its own order, interleaved with its other draws.
 
-    Returns (centres f32 [S*K, D], last assignment i32 [N] local to each segment)."""
+    Segment-parallel (``comm`` = distributed.Comm): every rank passes the same sizes,
+    limits and inits and X = the rows of ITS segments ``owned = (s0, s1)`` (contiguous ranges in rank
+    order).  Each rank fits its own segments; the centres, iteration counts and empty-cluster events are
+    all-gathered and every rank takes the same restart decisions.  A rank's torch draws start from the
+    common state advanced by its guess of the lower ranks' draw count (last attempt's count), so the
+    stream positions are checked exactly as in one process.
+
+    Returns (centres f32 [S*K, D] of ALL segments, last assignment i32 local to each segment, for the
+    rows of X)."""
     dev = X.device
     sizes = np.asarray(sizes, dtype=np.int64)
     S, K = len(sizes), n_clusters
     limits = np.asarray(iter_limits, dtype=np.int64).reshape(S)
     off = np.concatenate([[0], np.cumsum(sizes)])
+    o0, o1 = (0, S) if comm is None else (int(owned[0]), int(owned[1]))
+    base = int(off[o0])  # X's first row is segment o0's first row
+    if X.shape[0] != off[o1] - off[o0]:
+        raise ValueError("fit_segments: rows do not match the owned segments")
     min_loss_mode = target_nodes_num is not None
     if min_loss_mode and (limits == 0).any():
         raise ValueError("fit_segments: fit_by_min_loss needs a finite iter_limit per segment")
     if not min_loss_mode and (inits is None or len(inits) != S):
         raise ValueError("fit_segments: fit needs each segment's drawn start")
     centers = torch.empty((S * K, X.shape[1]), dtype=torch.float32, device=dev)
-    last = torch.empty((max(int(off[-1]), 1),), dtype=torch.int32, device=dev)
+    last = torch.empty((max(X.shape[0], 1),), dtype=torch.int32, device=dev)
     torch_state = torch.get_rng_state()
-    start, restarts = 0, 0
+    start, restarts, guess = 0, 0, 0
     while start < S:
         stop = S if restarts <= max_restarts else start + 1
-        segs = range(start, stop)
         np_states, seg_inits = [], []
-        for s in segs:
+        for s in range(start, stop):
             if min_loss_mode:
                 np_states.append(np.random.get_state())
                 seg_inits.append([init_indices(int(sizes[s]), K) for _ in range(reinit_draws(limits[s]))])
             else:
                 seg_inits.append(inits[s])
+        m0, m1 = max(start, o0), min(stop, o1)  # this rank's segments of the window
         torch.set_rng_state(torch_state)
-        layout = ops.SegmentLayout(sizes[start:stop], dev)
-        xs = X[int(off[start]):int(off[stop])].contiguous()
-        c, a, info = batched_fit(xs, layout, K, limits[start:stop], seg_inits, target_nodes_num=target_nodes_num,
-                                 tol=tol, half=half, return_info=True)
+        if guess:
+            torch.randint(2, (guess,))
+        iters = np.zeros(0, dtype=np.int64)
+        ev = np.zeros((0, 2), dtype=np.int64)  # (segment, stream position) in this rank's draw order
+        c_mine = torch.empty((0, X.shape[1]), dtype=torch.float32, device=dev)
+        if m1 > m0:
+            layout = ops.SegmentLayout(sizes[m0:m1], dev)
+            xs = X[int(off[m0]) - base:int(off[m1]) - base].contiguous()
+            c_mine, a, info = batched_fit(xs, layout, K, limits[m0:m1], seg_inits[m0 - start:m1 - start],
+                                          target_nodes_num=target_nodes_num, tol=tol, half=half, return_info=True)
+            last[int(off[m0]) - base:int(off[m1]) - base] = a
+            iters = np.asarray(info["iterations"], dtype=np.int64)
+            ev = np.asarray([(m0 + e[0], guess + t) for t, e in enumerate(info["events"])],
+                            dtype=np.int64).reshape(-1, 2)
+        if comm is not None:
+            c = comm.all_gather_rows(c_mine)
+            iters = comm.all_gather_rows(torch.from_numpy(iters)).numpy()
+            ev_all = [e.numpy() for e in comm.all_gather_list(torch.from_numpy(ev))]
+        else:
+            c, ev_all = c_mine, [ev]
         # numpy: the first segment that drew re-initialisations it never used
         bad_np, used = stop, None
         if min_loss_mode:
             for i in range(stop - start):
-                u = reinit_draws(max(int(info["iterations"][i]), 1))
+                u = reinit_draws(max(int(iters[i]), 1))
                 if u < len(seg_inits[i]):
                     bad_np, used = start + i, u
                     break
-        # torch: the first segment with a draw outside the reference's (segment, iteration) order
-        ev = [start + e[0] for e in info["events"]]
-        ref = sorted(range(len(ev)), key=lambda t: ev[t])
-        wrong = [ev[t] for p, t in enumerate(ref) if t != p]
-        bad_torch = min(wrong) if wrong else stop
+        # torch: the reference's stream position of every draw is its rank in (segment, draw order)
+        allev = np.concatenate(ev_all, 0)
+        order = np.argsort(allev[:, 0], kind="stable")
+        wrong = allev[order[allev[order, 1] != np.arange(len(order))], 0]
+        bad_torch = int(wrong.min()) if len(wrong) else stop
         good = min(bad_np + 1, bad_torch, stop)
         centers[start * K:good * K] = c[:(good - start) * K]
-        last[int(off[start]):int(off[good])] = a[:int(off[good] - off[start])]
         # the generators' state after the kept segments, as the reference leaves it
         if min_loss_mode:
             if good == bad_np + 1:
@@ -425,10 +452,12 @@ def fit_segments(X: torch.Tensor, sizes, n_clusters: int, iter_limits, inits=Non
             elif good < stop:
                 np.random.set_state(np_states[good - start])
         torch.set_rng_state(torch_state)
-        for seg in sorted(e for e in ev if e < good):
+        for seg in np.sort(allev[:, 0][allev[:, 0] < good]):
             torch.randint(int(sizes[seg]), (1,))
         torch_state = torch.get_rng_state()
+        # next attempt: this rank's draws start after the lower ranks' draws of segments >= good
+        guess = int(sum(int((e[:, 0] >= good).sum()) for r, e in enumerate(ev_all) if comm is not None and r < comm.rank))
         if good < stop:
             restarts += 1
         start = good
-    return centers, last[:int(off[-1])]
+    return centers, last[:X.shape[0]]

@@ -25,6 +25,95 @@ import torch.distributed as dist
 from . import ops
 
 
+class Comm:
+    """The collectives of the sharded trainer over one torch.distributed group.  RCCL ("nccl") reduces
+    device tensors in place; gloo (the CPU test backend, also used for several ranks sharing one GPU in
+    the GPU tests) stages device tensors through host memory.  Variable-size gathers exchange the
+    sizes first and pad to the largest share."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.stage = dist.get_backend(group) == "gloo"
+
+    def _host(self, t: torch.Tensor) -> torch.Tensor:
+        """The tensor the backend can take: host memory for gloo, device memory for RCCL."""
+        if self.stage:
+            return t.cpu() if t.is_cuda else t
+        return t if t.is_cuda else t.to(torch.device("cuda", torch.cuda.current_device()))
+
+    def all_reduce(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+        h = self._host(t.contiguous())
+        dist.all_reduce(h, op=op, group=self.group)
+        if h is not t:
+            t.copy_(h)
+        return t
+
+    def _sizes(self, n: int, device: torch.device):
+        t = self._host(torch.tensor([n], dtype=torch.int64))
+        parts = [torch.zeros_like(t) for _ in range(self.world)]
+        dist.all_gather(parts, t, group=self.group)
+        return [int(p.item()) for p in parts]
+
+    def all_gather_list(self, t: torch.Tensor):
+        """Every rank's tensor (first dimensions may differ), in rank order, on t's device."""
+        t = t.contiguous()
+        sizes = self._sizes(t.shape[0], t.device)
+        width = max(sizes)
+        src = self._host(t)
+        pad = torch.zeros((width,) + tuple(t.shape[1:]), dtype=t.dtype, device=src.device)
+        pad[:t.shape[0]] = src
+        parts = [torch.zeros_like(pad) for _ in range(self.world)]
+        dist.all_gather(parts, pad, group=self.group)
+        return [p[:m].to(t.device) for p, m in zip(parts, sizes)]
+
+    def all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenation over ranks (rank order) of every rank's rows."""
+        return torch.cat(self.all_gather_list(t), 0)
+
+    def all_to_all_rows(self, t: torch.Tensor, send_counts) -> torch.Tensor:
+        """Rows t[offsets of send_counts[r]] go to rank r; returns the rows received, in rank order."""
+        send_counts = [int(c) for c in send_counts]
+        sc = self._host(torch.tensor(send_counts, dtype=torch.int64))
+        rc = torch.zeros_like(sc)
+        dist.all_to_all_single(rc, sc, group=self.group)
+        recv = [int(c) for c in rc.cpu()]
+        src = self._host(t.contiguous())
+        out = torch.empty((sum(recv),) + tuple(t.shape[1:]), dtype=t.dtype, device=src.device)
+        dist.all_to_all_single(out, src, recv, send_counts, group=self.group)
+        return out.to(t.device)
+
+
+def balanced_ranges(sizes, world: int):
+    """Contiguous segment ranges [bounds[r], bounds[r+1]) per rank with about equal rows (segments stay
+    whole: the sub-fits of one parent / group are independent of the others)."""
+    sizes = np.asarray(sizes, dtype=np.int64)
+    cum = np.concatenate([[0], np.cumsum(sizes)])
+    total = cum[-1]
+    bounds = [0]
+    for r in range(1, world):
+        bounds.append(int(max(bounds[-1], np.searchsorted(cum, total * r / world, side="left"))))
+    bounds.append(len(sizes))
+    return np.asarray(bounds, dtype=np.int64)
+
+
+def regroup_rows(comm: "Comm", x_local: torch.Tensor, keys_local: torch.Tensor, bounds, extra=None):
+    """Send every local row to the rank owning its segment (keys in [bounds[r], bounds[r+1]) -> rank r);
+    returns the received rows in segment order, rows of one segment in ascending global row order (the
+    order of torch.where(ids == g) / group_rows in one process), plus any ``extra`` per-row tensors
+    regrouped the same way."""
+    keys = keys_local.long()
+    owner = torch.bucketize(keys, torch.as_tensor(bounds[1:-1], dtype=torch.int64, device=keys.device), right=True)
+    order = torch.sort(owner, stable=True)[1]
+    counts = torch.bincount(owner, minlength=comm.world).cpu().tolist()
+    send = [x_local[order]] + [e[order] for e in (extra or [])] + [keys[order]]
+    recv = [comm.all_to_all_rows(t, counts) for t in send]
+    k = recv[-1]
+    perm = torch.sort(k, stable=True)[1]  # sources arrive in rank order = ascending global row order
+    return [r[perm] for r in recv]
+
+
 def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
     """Contiguous row block of ``rank`` (the first ``n % world`` ranks get one extra row)."""
     base, extra = divmod(n, world)
@@ -42,19 +131,21 @@ def _gpu_accumulate(x: torch.Tensor, a: torch.Tensor, k: int):
 
 
 class ShardedLloyd:
-    """K-Means (``KMeans.fit``, balancekmeans/__init__.py:368-465) over row shards: unbalanced (nearest
-    centre) or, with ``balanced``, the reference's training assignment through a row-sharded auction
-    (ShardedAuction).  ``x_local`` holds rows [start, stop) of the global matrix of ``n_global`` rows."""
+    """K-Means (``KMeans.fit`` / ``KMeans.fit_by_min_loss``, balancekmeans/__init__.py:259-465) over row
+    shards: unbalanced (nearest centre) or, with ``balanced``, the reference's training assignment through
+    a row-sharded auction (ShardedAuction).  ``x_local`` holds rows [start, stop) of the global matrix of
+    ``n_global`` rows.  Every rank ends every iteration with bit-identical centres and takes the same
+    decisions (shift, min-loss bookkeeping, RNG draws) as the single-process fit."""
 
     def __init__(self, n_clusters: int, x_local: torch.Tensor, n_global: int, group=None,
                  assign_fn: Optional[Callable] = None, accumulate_fn: Optional[Callable] = None,
-                 balanced: bool = False, half: bool = False):
+                 balanced: bool = False, half: bool = False, nearest_fn: Optional[Callable] = None):
         self.k = n_clusters
         self.x = x_local
         self.n = n_global
         self.group = group
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
+        self.comm = Comm(group)
+        self.rank, self.world = self.comm.rank, self.comm.world
         self.start, self.stop = shard_bounds(n_global, self.rank, self.world)
         if x_local.shape[0] != self.stop - self.start:
             raise ValueError(f"rank {self.rank}: expected rows [{self.start}, {self.stop}) of {n_global}")
@@ -62,6 +153,7 @@ class ShardedLloyd:
             # balanced (KMeans(balanced=True), the reference's training): the row-sharded auction
             assign_fn = (lambda x, c: sharded_balanced_assign(x, c, n_global, half, group)) if balanced else _gpu_assign
         self.assign_fn = assign_fn
+        self.nearest_fn = nearest_fn or _gpu_assign
         self.accumulate_fn = accumulate_fn or _gpu_accumulate
         self.cluster_centers = None
 
@@ -73,18 +165,19 @@ class ShardedLloyd:
             pos = torch.from_numpy(np.nonzero(own)[0]).to(self.x.device)
             src = torch.from_numpy(idx[own] - self.start).to(self.x.device)
             buf[pos] = self.x[src].double()
-        dist.all_reduce(buf, group=self.group)
+        self.comm.all_reduce(buf)
         return buf.to(self.x.dtype)
 
     def initialize(self) -> torch.Tensor:
+        """KMeans.initialize (:240-256): the same np.random.choice draw on every rank."""
         replace = self.k > self.n
-        return self._rows(np.asarray(np.random.choice(self.n, self.k, replace=replace)))
+        return self._rows(np.asarray(np.random.choice(self.n, self.k, replace=replace))).contiguous()
 
     def step(self, centers: torch.Tensor):
         a = self.assign_fn(self.x, centers)
         sums, counts = self.accumulate_fn(self.x, a, self.k)
         buf = torch.cat([sums.reshape(-1), counts.reshape(-1).to(sums.dtype)])
-        dist.all_reduce(buf, group=self.group)
+        self.comm.all_reduce(buf)
         d = self.x.shape[1]
         sums, counts = buf[: self.k * d].reshape(self.k, d), buf[self.k * d:]
         new = centers.clone()
@@ -95,20 +188,51 @@ class ShardedLloyd:
             # the reference's per-cluster loop draws torch.randint(len(X), (1,)) for each empty cluster
             draws = np.asarray([int(torch.randint(self.n, (1,)).item()) for _ in empty])
             new[torch.tensor(empty, device=new.device)] = self._rows(draws)
-        return new, a, counts
+        return new.contiguous(), a, counts
+
+    @staticmethod
+    def _shift(c: torch.Tensor, prev: torch.Tensor) -> float:
+        """KMeans._shift / the reference's center_shift (:343-348), in fp32 like the single-process fit."""
+        return float(torch.sum(torch.sqrt(torch.sum((c - prev) ** 2, dim=1))).item())
 
     def fit(self, tol: float = 1e-3, iter_limit: int = 0):
+        """KMeans.fit (:368-465).  Returns this rank's last assignment."""
         centers = self.initialize()
         it = 0
         while True:
             prev = centers
             centers, a, _ = self.step(centers)
-            shift = float(torch.sum(torch.sqrt(torch.sum((centers.double() - prev.double()) ** 2, dim=1))).item())
+            shift = self._shift(centers, prev)
             it += 1
             if shift ** 2 < tol or (iter_limit != 0 and it >= iter_limit):
                 break
         self.cluster_centers = centers
         return a
+
+    def fit_by_min_loss(self, target_nodes_num, tol: float = 1e-3, iter_limit: int = 0):
+        """KMeans.fit_by_min_loss (:259-365): re-initialised every 10 iterations; after each update the
+        global nearest-centre histogram (one all_reduce of K counts) gives the overflow
+        loss sum(max(0, count - target)); the centres of the smallest loss (the latest of equal ones) win."""
+        centers = self.initialize()
+        it = 0
+        min_loss, best = float("inf"), None
+        while True:
+            if it > 0 and it % 10 == 0:
+                centers = self.initialize()
+            prev = centers
+            centers, _, _ = self.step(centers)
+            hist = torch.bincount(self.nearest_fn(self.x, centers).long().reshape(-1), minlength=self.k)
+            hist = self.comm.all_reduce(hist.to(torch.int64))
+            over = hist - target_nodes_num
+            cur_loss = float(over[over > 0].sum().item()) if bool((over > 0).any()) else 0
+            if cur_loss <= min_loss:
+                min_loss, best = cur_loss, centers.clone()
+            shift = self._shift(centers, prev)
+            it += 1
+            if shift ** 2 < tol or (iter_limit != 0 and it >= iter_limit):
+                break
+        self.cluster_centers = best
+        return None
 
 
 # ----------------------------------------------------------------------------------------------------

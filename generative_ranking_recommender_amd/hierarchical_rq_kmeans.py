@@ -269,7 +269,10 @@ class HierarchicalRQKMeans:
 
     # ------------------------------------------------------------------------------------ training
     def train(self, X: np.ndarray, resume: bool = True) -> Dict:
-        """:368-537."""
+        """:368-537.  With a process group (``group=``) the rows are sharded across the ranks: see
+        ``_train_sharded``."""
+        if self.group is not None:
+            return self._train_sharded(X, resume)
         cfg = self.config
         if X.shape[1] != cfg.embedding_dim:
             raise ValueError(f"Input dimension {X.shape[1]} does not match config embedding_dim {cfg.embedding_dim}")
@@ -286,6 +289,9 @@ class HierarchicalRQKMeans:
             ck = self.checkpoint_manager.load_layer_checkpoint(start_layer - 1, self.device)
             if ck and "residual_data" in ck:
                 current = ck["residual_data"].float().contiguous()
+            else:  # a sharded run's checkpoints hold no residuals: rebuild the chain from ids + centres
+                current = self._residual_chain(current, [t.to(self.device).long() for t in self.result_cluster_ids],
+                                               start_layer)
         for layer in range(start_layer, L):
             t0 = time.time()
             n_clusters, need = cfg.layer_clusters[layer], cfg.need_clusters[layer]
@@ -559,6 +565,223 @@ class HierarchicalRQKMeans:
                                                  np.full(len(full), need))
         return match
 
+    # ------------------------------------------------------------------------------ sharded training
+    def _train_sharded(self, X: np.ndarray, resume: bool) -> Dict:
+        """The same training, one process per GPU, every rank holding the same X (the CSV
+        is read by every rank; only rows [start, stop) of this rank are copied to its GPU):
+        * level 0 (balanced fit_by_min_loss): row-sharded Lloyd (distributed.ShardedLloyd) with the
+          row-sharded auction, one all_reduce of the fused [K*D + K] sums per iteration and one of the
+          K-bin nearest-centre histogram for the min-loss choice;
+        * middle level: segment-parallel -- the parents' rows are regrouped to the rank owning the parent
+          (one all_to_all), each rank runs its parents' sub-fits in lockstep (fit_segments with the
+          reference's RNG order checked across ranks) and the centres are all-gathered;
+        * last level: the two candidate fits row-sharded like level 0; the match-matrix groups
+          segment-parallel like the middle level (short groups' greedy rows gathered before the draw
+          loop every rank runs identically);
+        * reassignment and residuals on each rank's own rows; IDs all-gathered.
+        Every rank ends with the single-process model (centres, match matrix, IDs) and the same RNG
+        state; rank 0 alone writes checkpoints (resume recomputes the residual chain from them)."""
+        from .distributed import Comm, shard_bounds
+        cfg = self.config
+        if X.shape[1] != cfg.embedding_dim:
+            raise ValueError(f"Input dimension {X.shape[1]} does not match config embedding_dim {cfg.embedding_dim}")
+        comm = Comm(self.group)
+        self._comm = comm
+        n = len(X)
+        self._n_global = n
+        s0, s1 = shard_bounds(n, comm.rank, comm.world)
+        t_total = time.time()
+        L = len(cfg.layer_clusters)
+        current = torch.from_numpy(np.ascontiguousarray(X[s0:s1], dtype=np.float32)).to(self.device)
+        self._local_ids = []
+        start_layer = 0
+        if resume and self.checkpoint_manager:
+            start_layer = self.checkpoint_manager.get_last_completed_layer() + 1
+        start_layer = int(comm.all_reduce(torch.tensor([start_layer], dtype=torch.int64,
+                                                       device=self.device), op=torch.distributed.ReduceOp.MIN).item())
+        if start_layer > 0:
+            self._load_previous_checkpoints(start_layer)
+            self._local_ids = [t.to(self.device).long()[s0:s1] for t in self.result_cluster_ids[:start_layer]]
+            current = self._residual_chain(current, self._local_ids, start_layer)
+        for layer in range(start_layer, L):
+            t0 = time.time()
+            n_clusters, need = cfg.layer_clusters[layer], cfg.need_clusters[layer]
+            weighted = self._apply_weights(current, layer)
+            match = None
+            if n_clusters == need:
+                centers, ids, residual = self._train_layer_0_sharded(weighted, layer, n)
+            elif layer == L - 1:
+                centers, ids, residual = self._train_last_layer_sharded(weighted, layer, n)
+                match = self.match_matrices[-1]
+            else:
+                centers, ids, residual = self._train_middle_layer_sharded(weighted, layer)
+            self._local_ids.append(ids)
+            full = comm.all_gather_rows(ids.long())
+            self.cluster_centers_list.append(centers)
+            self.result_cluster_ids.append(full)
+            if self.checkpoint_manager and comm.rank == 0:
+                self.checkpoint_manager.save_layer_checkpoint(layer, full, None, centers, match)
+            if layer < L - 1:
+                current = residual
+            logger.info("[LAYER %d] completed in %.2fs (rank %d of %d)", layer + 1, time.time() - t0, comm.rank,
+                        comm.world)
+        self.is_trained = True
+        if self.checkpoint_manager and comm.rank == 0:
+            self.checkpoint_manager.save_metadata({
+                "num_layers": L, "embedding_dim": cfg.embedding_dim, "group_dims": cfg.group_dims,
+                "hierarchical_weights": cfg.hierarchical_weights, "num_samples": n, "world_size": comm.world})
+        logger.info("[TRAINING COMPLETE] Total time: %.2fs", time.time() - t_total)
+        return {"cluster_ids": self.result_cluster_ids, "cluster_centers": self.cluster_centers_list}
+
+    def _residual_chain(self, x: torch.Tensor, ids: List[torch.Tensor], n_layers: int) -> torch.Tensor:
+        """The training residual after ``n_layers`` completed levels, from their IDs and centres: level 0
+        subtracts c0[id0], a middle level its raw block id parent * need + id (:839-904)."""
+        cfg = self.config
+        cur = x
+        for layer in range(min(n_layers, len(cfg.layer_clusters) - 1)):
+            w = self._apply_weights(cur, layer)
+            raw = ids[0] if layer == 0 else ids[layer - 1] * cfg.need_clusters[layer] + ids[layer]
+            cur = self._compute_residuals_with_centers(w, raw, self.cluster_centers_list[layer].float())
+        return cur
+
+    def _train_layer_0_sharded(self, X: torch.Tensor, layer: int, n: int):
+        """:606-669 over row shards."""
+        from .distributed import ShardedLloyd
+        cfg = self.config
+        n_clusters = cfg.layer_clusters[layer]
+        target = 1
+        for idx, v in enumerate(cfg.need_clusters):
+            if idx != layer:
+                target *= v
+        iters = adaptive_iter_limit(n, n_clusters, layer, cfg.iter_limit)
+        sl = ShardedLloyd(n_clusters, X.contiguous(), n, group=self.group, balanced=True, half=n_clusters >= 512)
+        sl.fit_by_min_loss(target, iter_limit=iters)
+        centers = sl.cluster_centers.detach().contiguous()
+        ids = ops.nearest(X.contiguous(), ops.prepare_centers(centers)).long()
+        return centers, ids, self._compute_residuals_with_centers(X, ids, centers)
+
+    def _segment_owners(self, keys_local: torch.Tensor, n_segments: int):
+        """Global segment sizes (one all_reduce) and the contiguous segment ranges of the ranks."""
+        from .distributed import balanced_ranges
+        cnt = torch.bincount(keys_local.long(), minlength=n_segments).to(torch.int64)
+        sizes = self._comm.all_reduce(cnt).cpu().numpy().astype(np.int64)
+        return sizes, balanced_ranges(sizes, self._comm.world)
+
+    def _train_middle_layer_sharded(self, X: torch.Tensor, layer: int):
+        """:671-752, segment-parallel sub-fits."""
+        from .distributed import regroup_rows
+        cfg = self.config
+        comm = self._comm
+        cur_need, pre_need = cfg.need_clusters[layer], cfg.need_clusters[layer - 1]
+        prev = self._local_ids[layer - 1]
+        target = 1
+        for idx, v in enumerate(cfg.need_clusters):
+            if idx > layer:
+                target *= v
+        sizes, bounds = self._segment_owners(prev, pre_need)
+        xs, _ = regroup_rows(comm, X.contiguous(), prev, bounds)
+        limits = [adaptive_iter_limit(int(n_i), cur_need, layer, cfg.iter_limit, is_sub_cluster=True) for n_i in sizes]
+        t0 = time.time()
+        centers, _ = fit_segments(xs.contiguous(), sizes, cur_need, limits, target_nodes_num=target,
+                                  half=cur_need >= 512, comm=comm, owned=(bounds[comm.rank], bounds[comm.rank + 1]))
+        logger.info("[LAYER %d] %d segment-parallel sub-fits %.2fs", layer + 1, pre_need, time.time() - t0)
+        raw, residual = self._reassign_clusters_middle_layer_with_residuals(X, centers.contiguous(), prev, layer)
+        return centers.contiguous(), raw % cur_need, residual
+
+    def _train_last_layer_sharded(self, X: torch.Tensor, layer: int, n: int):
+        """:754-837: row-sharded candidate fits, segment-parallel match matrix."""
+        from .distributed import ShardedLloyd
+        cfg = self.config
+        n_clusters, need = cfg.layer_clusters[layer], cfg.need_clusters[layer]
+        if len(self._local_ids) < 2:
+            raise RuntimeError(
+                f"Previous layers cluster IDs not found. "
+                f"Expected at least 2 layers but only have {len(self._local_ids)} layers.")
+        parts = []
+        t0 = time.time()
+        for _ in range(2):
+            sl = ShardedLloyd(n_clusters, X.contiguous(), n, group=self.group, balanced=True,
+                              half=n_clusters >= 512)
+            sl.fit(iter_limit=20)
+            parts.append(sl.cluster_centers.detach())
+        cand = torch.cat(parts, 0).contiguous()
+        logger.info("[LAYER %d] row-sharded candidate fits %.2fs", layer + 1, time.time() - t0)
+        l1, l2 = self._local_ids[-2], self._local_ids[-1]
+        pp_need = cfg.need_clusters[layer - 2]
+        match = self._match_matrix_sharded(cand, X, cfg.need_clusters[layer - 1], l1, l2, pp_need, need, 2 * need, layer)
+        self.match_matrices.append(match)
+        before = l1 * pp_need + l2
+        raw, residual = self._reassign_clusters_last_layer_with_residuals(X, cand, before, match, layer)
+        ids = self._merge_match_matrix_cluster_ids(match, raw, before)
+        return cand, ids, residual
+
+    def _match_matrix_sharded(self, cand, X, prev_need, l1, l2, pp_need, need, trunc, layer) -> np.ndarray:
+        """_assign_last_match_matrix (:968-1053) with the (l1, l2) groups owned by ranks (contiguous
+        ranges); the draw loop over groups runs identically on every rank."""
+        from .distributed import regroup_rows
+        comm = self._comm
+        G = pp_need * prev_need
+        gid = l1.long() * prev_need + l2.long()
+        sizes, bounds = self._segment_owners(gid, G)
+        o0, o1 = int(bounds[comm.rank]), int(bounds[comm.rank + 1])
+        xs, _ = regroup_rows(comm, X.contiguous(), gid, bounds)
+        goff = np.concatenate([[0], np.cumsum(sizes[o0:o1])])  # row offsets of my groups in xs
+        n_cand = cand.shape[0]
+        match = np.zeros((G, n_cand), dtype=np.uint8)
+
+        def rows(g, picks=None):
+            a = int(goff[g - o0])
+            idx = np.arange(int(sizes[g])) if picks is None else np.asarray(picks)
+            return torch.from_numpy(a + idx.astype(np.int64)).to(self.device)
+
+        def greedy_rows(groups, centers_list, counts):
+            if not groups:
+                return torch.zeros((0, n_cand), dtype=torch.uint8, device=self.device)
+            sub_off = torch.tensor(np.concatenate([[0], np.cumsum(counts)]), dtype=torch.int32, device=self.device)
+            sc = torch.cat(centers_list, 0).float().contiguous()
+            r, _ = ops.greedy_match(ops.pairwise_distance(sc, cand), sub_off, need)
+            return r.to(torch.uint8)
+
+        def gather_rows(groups, r):
+            g_all = comm.all_gather_rows(torch.tensor(groups, dtype=torch.int64, device=self.device))
+            r_all = comm.all_gather_rows(r)
+            if len(g_all):
+                match[g_all.cpu().numpy()] = r_all.cpu().numpy()
+
+        short = [g for g in range(o0, o1) if 0 < sizes[g] < need]
+        gather_rows(short, greedy_rows(short, [xs[rows(g)] for g in short], [int(sizes[g]) for g in short]))
+        small, small_picks, big, big_inits = [], [], [], []
+        for g in range(G):  # the reference's draw order, on every rank
+            n_g = int(sizes[g])
+            if n_g == 0:
+                continue
+            if n_g < need:
+                random_fill(match[g], need)
+            elif n_g == need:
+                small.append(g)
+                small_picks.append(np.arange(n_g))
+            elif n_g < trunc:
+                small.append(g)
+                small_picks.append(np.asarray(np.random.choice(n_g, need, replace=False)))
+            else:
+                big.append(g)
+                big_inits.append([init_indices(n_g, need)])
+        centers = {}
+        for g, pk in zip(small, small_picks):
+            if o0 <= g < o1:
+                centers[g] = xs[rows(g, pk)]
+        if big:
+            bsz = sizes[big]
+            b0, b1 = int(np.searchsorted(big, o0)), int(np.searchsorted(big, o1))  # my big groups
+            xb = xs[torch.cat([rows(big[i]) for i in range(b0, b1)])] if b1 > b0 else xs[:0]
+            limits = [adaptive_iter_limit(int(v), need, layer, base_iter_limit=20) for v in bsz]
+            bc, _ = fit_segments(xb.contiguous(), bsz, need, limits, big_inits, half=False, comm=comm, owned=(b0, b1))
+            for i in range(b0, b1):
+                centers[big[i]] = bc[i * need:(i + 1) * need]
+        full = sorted(centers)
+        gather_rows(full, greedy_rows(full, [centers[g] for g in full], [need] * len(full)))
+        return match
+
     def _load_previous_checkpoints(self, start_layer: int):
         """:1307-1337."""
         for layer in range(start_layer):
@@ -580,25 +803,61 @@ class HierarchicalRQKMeans:
         """:539-581 -> int64 [N, L].  reference_quirks=True reproduces the reference exactly: middle-layer
         residuals use the modulo id (:1143) and the last layer looks up ``match_matrices[layer-1]`` (:1248),
         which does not exist for 3 layers, so its ids are unconstrained raw candidate indices.
-        reference_quirks=False gives the training-consistent encode (raw-id residuals, match lookup)."""
+        reference_quirks=False gives the training-consistent encode (raw-id residuals, match lookup).
+        With a process group the rows are sharded: each rank encodes rows [start, stop) on its GPU
+        (``encode_shard``, no collective) and the int32 IDs are all-gathered (SURVEY.md §8e encode)."""
         if not self.is_trained or not self.cluster_centers_list:
             raise RuntimeError("Model not trained. Call train() first or load a trained model.")
         cfg = self.config
         if X.shape[1] != cfg.embedding_dim:
             raise ValueError(f"Input dimension {X.shape[1]} does not match config embedding_dim {cfg.embedding_dim}")
+        if self.group is not None:
+            from .distributed import Comm, shard_bounds
+            comm = Comm(self.group)
+            s0, s1 = shard_bounds(len(X), comm.rank, comm.world)
+            x = torch.from_numpy(np.ascontiguousarray(X[s0:s1], dtype=np.float32)).to(self.device)
+            return self.gather_ids(self.encode_shard(x, reference_quirks)).cpu().numpy().astype(np.int64)
+        x = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to(self.device)
+        return self.encode_shard(x, reference_quirks).cpu().numpy().astype(np.int64)
+
+    def _encoder(self, reference_quirks: bool):
+        """The fused encoder of the trained codebooks (cached per semantics; rebuilt after training or
+        loading changes the codebooks)."""
         from .encode import LevelSemantics, RQEncoder
-        sem = LevelSemantics(match_lookup=not reference_quirks, residual_global_id=not reference_quirks)
+        key = (bool(reference_quirks), len(self.cluster_centers_list), len(self.match_matrices),
+               tuple(id(c) for c in self.cluster_centers_list))
+        cache = getattr(self, "_enc_cache", None)
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        cfg = self.config
         L = len(cfg.layer_clusters)
         match = None
         if L >= 3 and not reference_quirks:
             if not self.match_matrices:
                 raise RuntimeError("Model has no match matrix for the last layer.")
             match = torch.as_tensor(np.asarray(self.match_matrices[-1], dtype=np.uint8))
-        weights = cfg.hierarchical_weights
+        # training-consistent: raw block ids, the match lookup, residuals of the weighted rows (:442)
+        sem = LevelSemantics(match_lookup=not reference_quirks, residual_global_id=not reference_quirks,
+                             residual_from_weighted=not reference_quirks)
         enc = RQEncoder([c.float() for c in self.cluster_centers_list], cfg.need_clusters, match=match,
-                        group_dims=cfg.group_dims, weights=weights, semantics=sem, device=self.device)
-        x = torch.from_numpy(np.ascontiguousarray(X, dtype=np.float32)).to(self.device)
-        return enc.encode(x).cpu().numpy().astype(np.int64)
+                        group_dims=cfg.group_dims, weights=cfg.hierarchical_weights, semantics=sem, device=self.device)
+        self._enc_cache = (key, enc)
+        return enc
+
+    def encode_shard(self, x: torch.Tensor, reference_quirks: bool = False) -> torch.Tensor:
+        """Encode device-resident rows (this rank's shard): int32 [n, L] on the device.  The hot path of
+        ``predict`` and of bench.py (no host copies, no collective)."""
+        L = len(self.config.layer_clusters)
+        if x.shape[0] == 0:
+            return torch.zeros((0, L), dtype=torch.int32, device=self.device)
+        return self._encoder(reference_quirks).encode(x)
+
+    def gather_ids(self, ids_local: torch.Tensor) -> torch.Tensor:
+        """All ranks' IDs in row order (one variable-size all_gather of int32 rows)."""
+        if self.group is None:
+            return ids_local
+        from .distributed import Comm
+        return Comm(self.group).all_gather_rows(ids_local)
 
     # ------------------------------------------------------------------------------------ persistence
     def save_model(self, model_dir: str):

@@ -116,8 +116,12 @@ class SimplifiedHierarchicalRQ:
 
     def train(self, data_path: str, data_limit: int = None):
         """:176-245."""
-        cfg = self.config
         song_ids, emb = self._load_data(data_path, limit=data_limit)
+        return self.train_rows(song_ids, emb)
+
+    def train_rows(self, song_ids: List[str], emb: torch.Tensor):
+        """The body of train (:185-245) on rows already loaded (host or device tensor, fp32 or fp16)."""
+        cfg = self.config
         current = emb.float().to(self.device).contiguous()
         all_ids: Dict[str, List[int]] = {sid: [] for sid in song_ids}
         previous = None

@@ -62,8 +62,9 @@ class SemanticIDTrainer:
         max_samples = 100000 if self.use_test_config else None
         song_ids, vectors = self.load_song_vectors(max_samples=max_samples)
         vectors_np = np.asarray(vectors, dtype=np.float32) if vectors.dtype != np.float32 else vectors
-        model = HierarchicalRQKMeans(config=self.rqkmeans_config, checkpoint_dir=str(self.checkpoint_dir)
-                                     if self.rank == 0 else None, device=self.device, group=self.group)
+        # every rank reads the checkpoints on resume; only rank 0 writes them
+        model = HierarchicalRQKMeans(config=self.rqkmeans_config, checkpoint_dir=str(self.checkpoint_dir),
+                                     device=self.device, group=self.group)
         logger.info("Training status: %s", model.get_training_status())
         train_result = model.train(vectors_np, resume=resume)
         stats = None

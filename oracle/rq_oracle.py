@@ -289,7 +289,8 @@ def centroid_update(x: np.ndarray, assign: np.ndarray, centers: np.ndarray, rand
     return c
 
 
-def auction_lap_half(job_and_worker_to_score: np.ndarray, tie_rule: str = "torch") -> np.ndarray:
+def auction_lap_half(job_and_worker_to_score: np.ndarray, tie_rule: str = "torch",
+                     max_rounds: Optional[int] = None) -> np.ndarray:
     """balancekmeans/__init__.py:12-140 (return_token_to_worker=True), restated on fp16 numpy arrays.
 
     Every fp16 operation of the reference is reproduced with one rounding per op.  The one
@@ -298,7 +299,8 @@ def auction_lap_half(job_and_worker_to_score: np.ndarray, tie_rule: str = "torch
     delegates exactly those two selections to torch's CPU kernels (the third-party code the
     reference calls; torch 2.10.0 here), which pins the oracle to the reference on tied
     inputs too; ``tie_rule="stable"`` keeps the lowest job / worker index instead (the rule
-    the GPU kernels use, identical whenever the fp16 scores have no ties)."""
+    the GPU kernels use, identical whenever the fp16 scores have no ties).  ``max_rounds`` stops after
+    that many rounds and returns None (bench.py's bounded CPU-baseline sample only)."""
     s = np.asarray(job_and_worker_to_score, dtype=F32)
     num_jobs, num_workers = s.shape
     if num_jobs < num_workers:
@@ -350,6 +352,40 @@ def auction_lap_half(job_and_worker_to_score: np.ndarray, tie_rule: str = "torch
         index = high_bidders * num_jobs + jobs_with_bidder
         value.reshape(-1)[index] = w.reshape(-1)[index]
         counter += 1
+        if max_rounds is not None and counter >= max_rounds:
+            return None
+
+
+def auction_rounds_torch_cpu(job_and_worker_to_score: np.ndarray, rounds: int) -> float:
+    """Seconds per round of auction_lap_half (:12-140) on the host, with the reference's tensor operations
+    (torch CPU fp16: topk of jpw+1 per worker, bid scatter, retention overwrite, max over bidders, cost
+    and value update) -- the CPU-baseline leg of bench.py, which times ``rounds`` rounds of one auction
+    (the numpy restatement above is the checker; its per-round cost is ~20x torch's)."""
+    import time
+
+    import torch
+    w = torch.from_numpy(np.ascontiguousarray(np.asarray(job_and_worker_to_score, F32).T)).half()
+    k, n = w.shape
+    jpw = n // k
+    eps = max((w.max() - w.min()) / 50, torch.tensor(1e-4, dtype=torch.float16))
+    val = w.clone()
+    cost = torch.zeros(n, dtype=torch.float16)
+    keep = None
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        top_v, top_i = val.topk(jpw + 1, dim=1)
+        bid = torch.zeros_like(w)
+        bid.scatter_(1, top_i[:, :-1], (top_v[:, :-1] - top_v[:, -1:]) + eps)
+        if keep is not None:
+            bid.view(-1)[keep] = eps
+        has = (bid > 0).any(0)
+        jobs = has.nonzero().squeeze(1)
+        hb, hw = bid[:, jobs].max(dim=0)
+        cost[jobs] += hb
+        val = w - cost
+        keep = hw * n + jobs
+        val.view(-1)[keep] = w.view(-1)[keep]
+    return (time.perf_counter() - t0) / rounds
 
 
 def _auction_select(value: np.ndarray, jpw: int, tie_rule: str) -> np.ndarray:

@@ -275,3 +275,161 @@ def test_sharded_auction_matches_single_process(world, n, k, levels):
         assert rounds == 1002
     else:
         assert 1 <= rounds < 1002
+
+
+# ---- segment-parallel sub-fits: the exact-RNG machinery of balancekmeans.fit_segments ----------------
+def _stub_batched_fit(X, layout, n_clusters, iter_limits, inits, target_nodes_num=None, tol=1e-3, half=False,
+                      balanced=True, return_info=False):
+    """A CPU stand-in for the lockstep GPU loop with its RNG behaviour: segment s converges after
+    ``1 + size % 13`` iterations (early, before its budget, for most sizes), re-initialises from
+    inits[s][it // 10] at iterations 10, 20, ... (min-loss mode), and has 'empty clusters' (one
+    torch.randint(size) draw each) at iterations where (size + it) % 3 == 0, drawn in (iteration,
+    segment) order like batched_fit.  The 'centre' of a segment hashes everything it consumed."""
+    S = layout.n_seg
+    sizes = layout.sizes
+    limits = np.asarray(iter_limits).reshape(S)
+    it = np.zeros(S, dtype=np.int64)
+    conv = 1 + sizes % 13
+    acc = np.zeros(S)
+    for s in range(S):
+        acc[s] = float(np.sum(inits[s][0][:3]))
+    active = sizes > 0
+    events = []
+    while active.any():
+        for s in np.nonzero(active)[0]:
+            if target_nodes_num is not None and it[s] > 0 and it[s] % 10 == 0:
+                acc[s] += float(np.sum(inits[s][it[s] // 10][:3]))
+        for s in np.nonzero(active)[0]:
+            if (sizes[s] + it[s]) % 3 == 0:
+                v = int(torch.randint(int(sizes[s]), (1,)).item())
+                acc[s] = acc[s] * 1.000001 + v
+                events.append((int(s), int(it[s])))
+        it[active] += 1
+        active &= ~((it >= conv) | ((limits != 0) & (it >= limits)))
+    c = torch.from_numpy(np.repeat(acc, n_clusters)[:, None].repeat(2, 1)).float()
+    out = (c, torch.zeros(max(layout.n, 1), dtype=torch.int32))
+    return out + ({"iterations": it, "events": events},) if return_info else out
+
+
+def _stub_reference(sizes, k, limits, inits_fn, target):
+    """The reference's one-after-another loop with the stub's arithmetic, segment by segment."""
+    from generative_ranking_recommender_amd import ops
+    out = []
+    for s, n in enumerate(sizes):
+        inits = inits_fn(s) if inits_fn else None
+        lay = ops.SegmentLayout(np.array([n]), torch.device("cpu"))
+        if target is not None:  # draws happen as the fit advances: start, then one per 10 iterations used
+            conv = min(1 + n % 13, limits[s])
+            inits = [bk_init(n, k) for _ in range(1 + (conv - 1) // 10)]
+            inits += [inits[-1]] * 10
+        c, _, _ = _stub_batched_fit(None, lay, k, [limits[s]], [inits], target_nodes_num=target, return_info=True)
+        out.append(c)
+    return torch.cat(out)
+
+
+def bk_init(n, k):
+    from generative_ranking_recommender_amd.balancekmeans import init_indices
+    return init_indices(n, k)
+
+
+def _fs_worker(rank, world, port, sizes, k, limits, target, seed, out):
+    import generative_ranking_recommender_amd.balancekmeans as bk
+    from generative_ranking_recommender_amd.distributed import Comm, balanced_ranges
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bk.batched_fit = _stub_batched_fit
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    comm = Comm()
+    bounds = balanced_ranges(sizes, world)
+    o0, o1 = int(bounds[rank]), int(bounds[rank + 1])
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    xs = torch.zeros((int(off[o1] - off[o0]), 2))
+    inits = None if target is not None else [[bk.init_indices(int(n), k)] for n in sizes]
+    c, _ = bk.fit_segments(xs, sizes, k, limits, inits, target_nodes_num=target, comm=comm, owned=(o0, o1),
+                           max_restarts=2)
+    out.put((rank, c.numpy(), np.random.get_state()[1].copy(), torch.get_rng_state().numpy().copy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,target", [(2, 5), (3, 5), (2, None)])
+def test_segment_parallel_fits_keep_the_reference_rng_order(world, target, monkeypatch):
+    """fit_segments over ranks (segment-parallel, gloo) == in one process == the reference's sequential
+    loop, in results AND in the numpy / torch generator states afterwards, with early convergence
+    (unused re-initialisations) and empty-cluster draws in many segments (restarts forced)."""
+    import generative_ranking_recommender_amd.balancekmeans as bk
+    sizes = np.array([40, 7, 130, 22, 95, 61, 13, 300, 8], dtype=np.int64)
+    k, seed = 4, 21
+    limits = [25] * len(sizes) if target is not None else [6] * len(sizes)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fs_worker, args=(r, world, port, sizes, k, limits, target, seed, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    # one process (comm=None), and the sequential reference
+    monkeypatch.setattr(bk, "batched_fit", _stub_batched_fit)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    inits = None if target is not None else [[bk.init_indices(int(n), k)] for n in sizes]
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    c1, _ = bk.fit_segments(torch.zeros((int(off[-1]), 2)), sizes, k, limits, inits, target_nodes_num=target)
+    st1 = (np.random.get_state()[1].copy(), torch.get_rng_state().numpy().copy())
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    if target is None:
+        starts = [[bk.init_indices(int(n), k)] for n in sizes]
+        cref = _stub_reference(sizes, k, limits, lambda s: starts[s], None)
+    else:
+        cref = _stub_reference(sizes, k, limits, None, target)
+    stref = (np.random.get_state()[1].copy(), torch.get_rng_state().numpy().copy())
+    assert torch.equal(c1, cref)
+    assert np.array_equal(st1[0], stref[0]) and np.array_equal(st1[1], stref[1])
+    for rank, c, nps, ts in res:
+        assert np.array_equal(c, cref.numpy()), rank
+        assert np.array_equal(nps, stref[0]) and np.array_equal(ts, stref[1]), rank
+
+
+def _comm_worker(rank, world, port, out):
+    from generative_ranking_recommender_amd.distributed import Comm, regroup_rows
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Comm()
+    n = 50
+    s, e = shard_bounds(n, rank, world)
+    keys = torch.from_numpy(np.random.default_rng(3).integers(0, 6, n)[s:e])
+    rows = torch.arange(s, e, dtype=torch.float32)[:, None].repeat(1, 3)
+    bounds = np.array([0, 2, 6]) if world == 2 else np.array([0, 1, 3, 6])
+    xs, kk = regroup_rows(comm, rows, keys, bounds)
+    lst = comm.all_gather_list(torch.arange(rank + 1))
+    out.put((rank, xs.numpy(), kk.numpy(), [t.numpy() for t in lst]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_regroup_rows_orders_like_one_process(world):
+    """regroup_rows: every segment's rows land on its owner, segments in order, each segment's rows in
+    ascending global row order (= group_rows / torch.where in one process); variable all_gather."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    keys = np.random.default_rng(3).integers(0, 6, 50)
+    order = np.argsort(keys, kind="stable")
+    bounds = [0, 2, 6] if world == 2 else [0, 1, 3, 6]
+    got = np.concatenate([r[1][:, 0] for r in res])
+    assert np.array_equal(got, order.astype(np.float32))
+    for r, (_, xs, kk, lst) in enumerate(res):
+        assert ((kk >= bounds[r]) & (kk < bounds[r + 1])).all()
+        assert [len(t) for t in lst] == list(range(1, world + 1))

@@ -38,7 +38,9 @@ def test_auction_golden_inputs_match_oracle(golden, tag):
 # N % 4 == 0 takes the 8-byte-load sweeps (4 jobs per lane, ranks in lane-major job order); 4100 and 2048
 # add heavily tied multi-chunk cases of that path (tie ranks across lanes, waves and chunks)
 @pytest.mark.parametrize("n,k,levels", [(200, 8, 0), (256, 8, 0), (999, 16, 7), (3000, 16, 0), (513, 32, 3),
-                                        (4100, 16, 5), (2048, 8, 3), (3001, 16, 5)])
+                                        (4100, 16, 5), (2048, 8, 3), (3001, 16, 5),
+                                        # K = 256 (BASELINE configs[4]'s level 0 / middle level)
+                                        (5120, 256, 7), (5120, 256, 0), (601, 256, 5)])
 def test_auction_random_and_tied_match_oracle(n, k, levels):
     rng = np.random.default_rng(n * k)
     d = rng.random((n, k), dtype=np.float32) * 4
