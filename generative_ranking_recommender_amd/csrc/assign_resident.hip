@@ -67,6 +67,12 @@ constexpr int kNC = kCW * 32;            // candidate capacity
 #ifndef RQ_NT
 #define RQ_NT 1  // non-temporal row loads (read once)
 #endif
+#ifndef RQ_E1V2
+#define RQ_E1V2 0  // epilogue 1 as independent bounds + min trees (summary: least lb, second least lb, least ub)
+#endif
+#if RQ_E1V2 && !RQ_LBF16
+#error "RQ_E1V2 keeps the deferred lower bounds as bf16 pairs"
+#endif
 #ifndef RQ_LA
 #define RQ_LA 6  // k-steps of the centres kept in LDS (wave-private) instead of registers
 #endif
@@ -720,6 +726,63 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
         e2_pen = ti.pen;
         const float* csq = csq_base + ti.slot * kNC + 32 * cw + 4 * h;
         const float* cy = cy_base + ti.slot * kNC + 32 * cw + 4 * h;
+#if RQ_E1V2
+        // Summary {least lb, second least lb, least ub} with the candidate of the least lb: a row is
+        // definitive iff exactly one candidate of all waves has lb <= U' (epilogue 2), and that one is
+        // then the argmin of ub too (its own lb <= its ub = U), so this posts what epilogue 2 needs with
+        // independent bounds (no serial select chain) and three-level min trees.
+        float ubv[16], lbv[16];
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          if (g % (8 / RQ_E1R) == 0) __builtin_amdgcn_sched_barrier(0);
+          const float2 cs = *reinterpret_cast<const float2*>(csq + 8 * (g >> 1) + 2 * (g & 1));
+          const float2 yy = *reinterpret_cast<const float2*>(cy + 8 * (g >> 1) + 2 * (g & 1));
+          const float csv[2] = {cs.x, cs.y}, yv[2] = {yy.x, yy.y};
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int v = 2 * g + e;
+            const float P = fmaf(m2, acc[v], csv[e]);
+            const float E = fmaf(A2, yv[e], 1e-30f);
+            ubv[v] = P + E;
+            lbv[v] = P - E;
+          }
+          lbp[g] = bf16_down(lbv[2 * g]) | (bf16_down(lbv[2 * g + 1]) << 16);
+        }
+        float U = fminf(fminf(fminf(fminf(ubv[0], ubv[1]), ubv[2]), fminf(fminf(ubv[3], ubv[4]), ubv[5])),
+                        fminf(fminf(fminf(ubv[6], ubv[7]), ubv[8]), fminf(fminf(ubv[9], ubv[10]), ubv[11])));
+        U = fminf(U, fminf(fminf(ubv[12], ubv[13]), fminf(ubv[14], ubv[15])));
+        float l1[8], l2[8];
+        int ix[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float a0 = lbv[2 * i], a1 = lbv[2 * i + 1];
+          const bool lo = a0 <= a1;
+          l1[i] = fminf(a0, a1);
+          l2[i] = fmaxf(a0, a1);
+          ix[i] = lo ? 2 * i : 2 * i + 1;
+        }
+#pragma unroll
+        for (int w = 4; w >= 1; w >>= 1) {
+#pragma unroll
+          for (int i = 0; i < w; ++i) {
+            const bool lo = l1[i] <= l1[i + w];
+            l2[i] = fminf(fminf(fmaxf(l1[i], l1[i + w]), l2[i]), l2[i + w]);
+            l1[i] = fminf(l1[i], l1[i + w]);
+            ix[i] = lo ? ix[i] : ix[i + w];
+          }
+        }
+        float lbk = l1[0], Lo = l2[0];
+        int kpos = 32 * cw + (ix[0] & 3) + 8 * (ix[0] >> 2) + 4 * h;
+        const float oU = __shfl_xor(U, 32), ol1 = __shfl_xor(lbk, 32), ol2 = __shfl_xor(Lo, 32);
+        const int ok = __shfl_xor(kpos, 32);
+        const bool take = ol1 < lbk || (ol1 == lbk && ok < kpos);
+        Lo = fminf(fminf(fmaxf(lbk, ol1), Lo), ol2);
+        lbk = fminf(lbk, ol1);
+        kpos = take ? ok : kpos;
+        U = fminf(U, oU);
+        if (h == 0) ex_row[cw] = make_float4(lbk, Lo, U, 0.f);
+        if (h == 0) id_row[cw] = make_int2(cid_base[ti.slot * kNC + kpos], clid_base[ti.slot * kNC + kpos]);
+#else
         float U = INFINITY, lbk = INFINITY, Lo = INFINITY;
         int kv = 0;
 #pragma unroll
@@ -761,6 +824,7 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
         if (h == 0) ex_row[cw] = make_float4(lbk, Lo, U, 0.f);  // (lbk, Lo): an 8-B aligned pair
         // this wave's candidate ids, posted beside the summary for the tile's store wave
         if (h == 0) id_row[cw] = make_int2(cid_base[ti.slot * kNC + kpos], clid_base[ti.slot * kNC + kpos]);
+#endif
       }
       lds_publish(ctr_posted + cw, (uint32_t)(it + 1));
       RS_MARK(4);
