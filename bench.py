@@ -71,25 +71,36 @@ def parse():
     ap.add_argument("--parity-rows", type=int, default=2048,
                     help="rows of the timed output checked against the exact CPU oracle after the run (0 = skip)")
     a = ap.parse_args()
-    global NEED, N_CAND
+    global NEED, N_CAND, PRESET
+    PRESET = a.preset
     if a.preset == "xl":
         NEED, N_CAND = [256, 256, 512], 5120
+        if a.traffic_json == str(REPO / "bench_data" / "traffic.json"):
+            a.traffic_json = str(REPO / "bench_data" / "traffic_xl.json")
     if a.rows <= 0:
         a.rows = 6_250_000 if a.preset == "xl" else 10_000_000
     return a
 
 
-# kernels of each encode level's rqsid_assign call (per-tile screen + exact re-score; see encode.py)
-LEVEL_KERNELS = {0: ("assign_screen_kernel<4, 2, 0, false, false, true>", "assign_rescore_kernel<0, false>"),
-                 1: ("assign_screen_kernel<4, 2, 1, true, true, true>", "assign_rescore_kernel<1, true>"),
-                 2: ("assign_pp_kernel<8, 2, true, false>", "assign_rescore_kernel<2, true>")}
+# kernels of each encode level's rqsid_assign call under the default dispatch (assign.hip rqsid_assign:
+# screen + exact re-score), per preset
+LEVEL_KERNELS = {
+    "prod": {0: ("assign_screen_kernel<4, 2, 0, false, false, true>", "assign_rescore_kernel<0, false>"),
+             1: ("assign_screen_kernel<4, 2, 1, true, true, true>", "assign_rescore_kernel<1, true>"),
+             2: ("assign_pp_kernel<8, 2, true, false>", "assign_rescore_kernel<2, true>")},
+    # [256,256,512]: 256-candidate level 0 (ping-pong form), 256-candidate 3-term level 1 in two passes,
+    # 512-candidate level 2 (two-pass per-tile screen)
+    "xl": {0: ("assign_pp_kernel<8, 0, false, false>", "assign_rescore_kernel<0, false>"),
+           1: ("assign_screen_kernel<4, 2, 1, true, true, false>", "assign_rescore_kernel<1, true>"),
+           2: ("assign_screen_kernel<8, 2, 2, true, false, false>", "assign_rescore_kernel<2, true>")}}
+PRESET = "prod"
 
 
 def level_traffic(path, lvl):
     """HBM bytes (PMC FETCH_SIZE x2 + WRITE_SIZE) of one launch of level lvl's kernels, or None."""
     try:
         ks = json.load(open(path))["kernels"]
-        return sum(ks[k]["hbm_bytes"] for k in LEVEL_KERNELS[lvl])
+        return sum(ks[k]["hbm_bytes"] for k in LEVEL_KERNELS[PRESET][lvl])
     except (OSError, KeyError, TypeError, ValueError):
         return None
 
@@ -469,7 +480,7 @@ def main():
         kern["bucket"] = {"ms": round(ms["bucket"], 3)}
     dom = max((k for k in kern if k.startswith("assign")), key=lambda k: kern[k]["ms"])
     dk = kern[dom]
-    traffic = level_traffic(args.traffic_json, int(dom[-1])) if os.environ.get("RQSID_SCREEN_VARIANT", "0") == "0" and NEED == [128, 128, 256] else None
+    traffic = level_traffic(args.traffic_json, int(dom[-1])) if os.environ.get("RQSID_SCREEN_VARIANT", "0") == "0" else None
     # Which roof applies: the level's algorithmic intensity (2 K_eff D flop per 2052 B: 64-128 flop/B) puts
     # its fp16 MFMA time at <= 6 % of its HBM time at the two peaks, so HBM is the roof; the PMC traffic
     # (when present) says whether the kernel moves more than its algorithmic bytes.
