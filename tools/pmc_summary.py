@@ -31,7 +31,7 @@ def main(root):
             durs[k][(f, d)] = dur
     cols = ["dur_us", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "wait_any%", "wait_inst%", "active%",
             "SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_INSTS_VMEM", "mfma_busy%", "lds_conflict%",
-            "FETCH_bytes", "TCC_hit%", "clock_GHz"]
+            "FETCH_bytes", "WRITE_bytes", "TCC_hit%", "clock_GHz", "SQ_INSTS_SALU", "SQ_WAVES"]
     print("kernel," + ",".join(cols))
     for k, cs in sorted(per.items()):
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -45,7 +45,8 @@ def main(root):
                "SQ_INSTS_LDS": avg.get("SQ_INSTS_LDS"), "SQ_INSTS_VMEM": avg.get("SQ_INSTS_VMEM"),
                "mfma_busy%": 100 * avg.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / max(avg.get("GRBM_GUI_ACTIVE", 1) / 8 * 1024, 1),
                "lds_conflict%": 100 * avg.get("SQ_LDS_BANK_CONFLICT", 0) / max(avg.get("SQ_LDS_IDX_ACTIVE", 1), 1),
-               "FETCH_bytes": 2 * 1024 * avg.get("FETCH_SIZE", 0),
+               "FETCH_bytes": 2 * 1024 * avg.get("FETCH_SIZE", 0), "WRITE_bytes": 1024 * avg.get("WRITE_SIZE", 0),
+               "SQ_INSTS_SALU": avg.get("SQ_INSTS_SALU"), "SQ_WAVES": avg.get("SQ_WAVES"),
                "TCC_hit%": 100 * avg.get("TCC_HIT_sum", 0) / max(avg.get("TCC_HIT_sum", 0) + avg.get("TCC_MISS_sum", 0), 1),
                "clock_GHz": avg.get("GRBM_GUI_ACTIVE", 0) / 8 / (dur * 1e3) if dur else 0}
         print(k + "," + ",".join("" if row[c] is None else f"{row[c]:.4g}" for c in cols))
