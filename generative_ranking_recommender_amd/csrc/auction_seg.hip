@@ -30,7 +30,7 @@ constexpr int kKG = 16;        // workers per block
 constexpr int kCh = 1024;      // jobs per chunk
 constexpr int kJPT = kCh / 256;
 constexpr int kAbovePad = 32;  // u32 per worker in SegAuction::above
-static_assert(kJPT == 4 && kJPT * kKG == 64, "load_chunk<true> takes 4 jobs per lane; sa_bid_kernel keeps one deferral bit per (job slice, worker) in a u64, "
+static_assert(kJPT == 4 && kJPT * kKG == 64, "load_chunk<true> takes 4 jobs per lane; sa_bid_kernel keeps one deferral bit per (job slice, worker) in two u32, "
               "and its 64 x 4 eqm slots are zeroed by the 256 threads");
 
 __device__ __forceinline__ float h2f(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
@@ -83,8 +83,9 @@ struct SegAuction {
   uint32_t* above;               // [n_multi*K][kAbovePad] values with high byte > b1 (one line per worker:
                                  // every chunk block adds to it)
   uint8_t* miss;                 // [n_multi*K]
-  uint16_t* chist;               // [total_chunks][K][256] each chunk's low-byte histogram of bin b1 from the
+  uint16_t* chist;               // [K][total_chunks][256] each chunk's low-byte histogram of bin b1 from the
                                  // guessed pass: a hit worker's per-chunk tie count is entry T & 255
+  uint32_t* any_miss;            // [1] some worker missed this round (the two-pass kernels exit at once if not)
 };
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ off, int n_seg, int64_t i) {
@@ -299,28 +300,25 @@ __device__ __forceinline__ void wave_select(const uint32_t* __restrict__ h, uint
 }
 
 // multi-chunk segments: global histograms.  MODE 0: high bytes, 1: low bytes of the values in the
-// selected bin b1 (sel[0]), 2: low bytes of the values in last round's bin b1 (sel[0]) plus the count of
-// values above it (the guessed pass).  With the guessed pass on (a.miss), modes 0 and 1 run only for the
-// workers it missed.
+// selected bin b1 (sel[0]).  With the guessed pass on (a.miss), they run only for the workers it missed.
 template <int MODE, bool VEC>
 __global__ __launch_bounds__(256) void sa_hist_kernel(SegAuction a) {
+  if (a.any_miss && !*a.any_miss) return;
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
   if (!(f & kLive) || (f & kSingle)) return;
   __shared__ uint32_t h[kKG][256];
-  __shared__ uint32_t abv[kKG];
   const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
   const int lane = threadIdx.x & 63;
   const int64_t sw0 = (int64_t)ci.s * a.K + w0;
   const int64_t hw0 = (int64_t)a.hidx[ci.s] * a.K + w0;
   uint32_t part = (1u << nw) - 1u;  // workers taking this pass
-  if (MODE != 2 && a.miss) {
+  if (a.miss) {
     part = 0;
     for (int g = 0; g < nw; ++g) part |= (uint32_t)(a.miss[hw0 + g] != 0) << g;
     if (!part) return;
   }
   for (int i = threadIdx.x; i < kKG * 256; i += 256) (&h[0][0])[i] = 0;
-  if (threadIdx.x < kKG) abv[threadIdx.x] = 0;
   __syncthreads();
   // high-byte pass: a worker's values crowd into one or two high-byte bins, where same-address LDS
   // atomics serialise a wave 64-fold.  The bins at and just below last round's threshold (sel[0]; any
@@ -338,7 +336,6 @@ __global__ __launch_bounds__(256) void sa_hist_kernel(SegAuction a) {
       const uint32_t k = okey(value_bits(w0 + g, cs.v[t][g], cs.hb[t], cs.c[t]));
       if (MODE != 0) {
         if (live && (k >> 8) == b1[g]) atomicAdd(&h[g][k & 255], 1u);
-        if (MODE == 2) n0[g] += (uint32_t)__popcll(__ballot(live && (k >> 8) > b1[g]));
       } else {
         const uint32_t d = b1[g] - (k >> 8);  // 0: the guessed bin, 1: the bin below
         n0[g] += (uint32_t)__popcll(__ballot(live && d == 0));
@@ -353,28 +350,134 @@ __global__ __launch_bounds__(256) void sa_hist_kernel(SegAuction a) {
       if (n1[g]) atomicAdd(&h[g][b1[g] - 1], n1[g]);  // n1 > 0 implies b1 >= 1
     }
   }
-  if (MODE == 2 && lane == 0) {
-    for (int g = 0; g < nw; ++g)
-      if (n0[g]) atomicAdd(&abv[g], n0[g]);
-  }
   __syncthreads();
-  if (MODE == 2 && threadIdx.x < nw && abv[threadIdx.x]) atomicAdd(&a.above[(hw0 + threadIdx.x) * kAbovePad], abv[threadIdx.x]);
-  if (MODE == 2) {  // counts <= kCh fit 16 bits; one 8-byte store per 4 slots
-    uint16_t* dst = a.chist + ((int64_t)blockIdx.x * a.K + w0) * 256;
-    for (int i = threadIdx.x; i < nw * 64; i += 256) {
-      const uint32_t* q = &h[0][0] + 4 * i;
-      *reinterpret_cast<uint2*>(dst + 4 * i) = make_uint2(q[0] | (q[1] << 16), q[2] | (q[3] << 16));
-    }
-  }
   for (int i = threadIdx.x; i < nw * 256; i += 256) {
     const uint32_t c = (&h[0][0])[i];  // zero for the workers that did not take part
     if (c) atomicAdd(&a.hist[(hw0 + i / 256) * 256 + (i & 255)], c);
   }
 }
 
+// Per-lane view of one chunk for the branch-free sweeps: a lane past the chunk's end gets no winner and
+// the cost NaN, so every one of its values is NaN (neither above nor equal to any threshold) without a
+// per-value liveness test; the histogram pass also offsets its keys below every bin (dead).  A job's
+// value for worker w is r - c' with c' = -0 for the previous winner (its raw score r; r - -0 also turns
+// -0 into +0) and the job's cost otherwise: one fp16 subtraction, the reference's step (value_h).
+struct LaneJobs {
+  int32_t hb[kJPT];
+  _Float16 c[kJPT];
+  int32_t dead[kJPT];  // 0 or -0x20000
+};
+
+template <bool VEC>
+__device__ __forceinline__ LaneJobs lane_jobs(const ChunkInfo& ci, const ChunkScores& cs) {
+  LaneJobs lj;
+#pragma unroll
+  for (int t = 0; t < kJPT; ++t) {
+    const bool live = job_of<VEC>(t) < ci.nj;
+    lj.hb[t] = live ? cs.hb[t] : -1;
+    lj.c[t] = __builtin_bit_cast(_Float16, live ? cs.c[t] : (uint16_t)0x7E00u);
+    lj.dead[t] = live ? 0 : -0x20000;
+  }
+  return lj;
+}
+
+__device__ __forceinline__ _Float16 lane_value(int w, uint16_t v, int32_t hbj, _Float16 c) {
+  return __builtin_bit_cast(_Float16, v) - (hbj == w ? (_Float16)-0.0f : c);
+}
+
+// The guessed pass: per worker, the low-byte histogram of its values in last round's high-byte bin b1
+// (sel[0]) and the count of values above that bin, in one sweep with no ballots and no branches per value
+// other than the LDS atomic: d = okey(x) - (b1 << 8) is the bin slot (0..255), >= 256 above the bin (slot
+// 256), negative below.  Both the values in b1 and those above it are about 1/K of a worker's values, so
+// the predicated atomic is rare.  d comes from x's raw bits in one operation, by the sign of the bin's
+// values (uniform per worker): x = v + (0 - c) is never -0 (a round-to-nearest sum is -0 only when both
+// addends are), so okey(x) = bits | 0x8000 for x >= +0 and 0xFFFF - bits for x < 0, and
+//   a bin of values >= +0 (b1 >= 0x80): d = sext16(bits) + 0x8000 - base (every x < 0 lands below),
+//   a bin of values < 0:                d = 0xFFFF - base - bits (every x >= +0 lands above).
+// A lane past the chunk's end takes the cost +inf (x = -inf: below every bin of a finite threshold); a
+// threshold of -inf (b1 < 4) takes explicit dead offsets (DEAD).
+constexpr int kGStride = 260;  // LDS words per worker: 256 low-byte slots + the above count, padded to 16 B
+
+template <bool NEG, bool DEAD>
+__device__ __forceinline__ void guess_worker(const uint16_t (&v)[kJPT], const LaneJobs& lj, const _Float16 (&nc)[kJPT],
+                                             int w, int32_t addk, uint32_t* __restrict__ hg) {
+#pragma unroll
+  for (int t = 0; t < kJPT; ++t) {
+    const _Float16 x = __builtin_bit_cast(_Float16, v[t]) + (lj.hb[t] == w ? (_Float16)0.0f : nc[t]);
+    const uint32_t b = __builtin_bit_cast(uint16_t, x);
+    int32_t d = NEG ? addk - (int32_t)b : (int32_t)(int16_t)b + addk;
+    if (DEAD) d += lj.dead[t];
+    if (d >= 0) atomicAdd(&hg[min(d, 256)], 1u);
+  }
+}
+
+template <bool DEAD>
+__device__ __forceinline__ void guess_values(const ChunkScores& cs, const LaneJobs& lj, const _Float16 (&nc)[kJPT],
+                                             const int32_t (&addk)[kKG], uint32_t negbin, int w0, uint32_t* h) {
+#pragma unroll
+  for (int g = 0; g < kKG; ++g) {
+    const uint16_t v[kJPT] = {cs.v[0][g], cs.v[1][g], cs.v[2][g], cs.v[3][g]};
+    if ((negbin >> g) & 1u) guess_worker<true, DEAD>(v, lj, nc, w0 + g, addk[g], h + g * kGStride);
+    else guess_worker<false, DEAD>(v, lj, nc, w0 + g, addk[g], h + g * kGStride);
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void sa_guess_hist_kernel(SegAuction a) {
+  const ChunkInfo ci = chunk_info(a, blockIdx.x);
+  const uint8_t f = a.flag[ci.s];
+  if (!(f & kLive) || (f & kSingle)) return;
+  constexpr int kStride = kGStride;
+  __shared__ uint32_t h[kKG * kStride];
+  const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
+  const int64_t sw0 = (int64_t)ci.s * a.K + w0;
+  const int64_t hw0 = (int64_t)a.hidx[ci.s] * a.K + w0;
+  for (int i = threadIdx.x; i < kKG * kStride / 4; i += 256) reinterpret_cast<uint4*>(h)[i] = make_uint4(0, 0, 0, 0);
+  // workers past K: a bin of values >= +0 with every d negative
+  int32_t addk[kKG];
+  uint32_t negbin = 0;
+  bool low = false;  // some worker's bin holds -inf
+  for (int g = 0; g < kKG; ++g) {
+    addk[g] = -0x20000;
+    if (g >= nw) continue;
+    const int32_t base = (int32_t)((a.sel[(sw0 + g) * 4 + 0] & 255u) << 8);
+    if (base >= 0x8000) {
+      addk[g] = 0x8000 - base;
+    } else {
+      addk[g] = 0xFFFF - base;
+      negbin |= 1u << g;
+      low |= base < 0x400;
+    }
+  }
+  ChunkScores cs;
+  load_chunk<VEC>(a, ci, w0, cs);
+  const LaneJobs lj = lane_jobs<VEC>(ci, cs);
+  _Float16 nc[kJPT];
+#pragma unroll
+  for (int t = 0; t < kJPT; ++t) nc[t] = lj.dead[t] ? (_Float16)-INFINITY : (_Float16)0.0f - lj.c[t];
+  __syncthreads();
+  if (low && ci.nj < kCh) guess_values<true>(cs, lj, nc, addk, negbin, w0, h);
+  else guess_values<false>(cs, lj, nc, addk, negbin, w0, h);
+  __syncthreads();
+  if (threadIdx.x < nw && h[threadIdx.x * kStride + 256])
+    atomicAdd(&a.above[(hw0 + threadIdx.x) * kAbovePad], h[threadIdx.x * kStride + 256]);
+  // counts <= kCh fit 16 bits; one 8-byte store per 4 slots; worker-major, so a worker's per-chunk tie
+  // counts (eqscan) lie in one contiguous run
+  for (int i = threadIdx.x; i < nw * 64; i += 256) {
+    const uint32_t* q = &h[(i >> 6) * kStride + 4 * (i & 63)];
+    uint16_t* dst = a.chist + ((int64_t)(w0 + (i >> 6)) * a.total_chunks + blockIdx.x) * 256 + 4 * (i & 63);
+    *reinterpret_cast<uint2*>(dst) = make_uint2(q[0] | (q[1] << 16), q[2] | (q[3] << 16));
+  }
+  for (int i = threadIdx.x; i < nw * 256; i += 256) {
+    const uint32_t c = h[(i >> 8) * kStride + (i & 255)];
+    if (c) atomicAdd(&a.hist[(hw0 + (i >> 8)) * 256 + (i & 255)], c);
+  }
+}
+
 // one wave per (segment, worker) of the multi-chunk segments
 template <bool LOW>
 __global__ __launch_bounds__(256) void sa_select_kernel(SegAuction a) {
+  if (a.any_miss && !*a.any_miss) return;
   const int64_t hw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (hw >= (int64_t)a.n_multi * a.K) return;
   const int s = a.mseg[hw / a.K];
@@ -430,6 +533,7 @@ __global__ __launch_bounds__(256) void sa_select_guess_kernel(SegAuction a) {
       sel[3] = jpw - (ab + above);
     }
     a.miss[hw] = hit ? 0 : 1;
+    if (!hit) *a.any_miss = 1;
     a.above[hw * kAbovePad] = 0;
   }
   for (int i = lane; i < 256; i += 64) h[i] = 0;
@@ -493,6 +597,7 @@ __global__ __launch_bounds__(256) void sa_small_select_kernel(SegAuction a) {
 // ---- tie counts (multi-chunk segments) ----
 template <bool VEC>
 __global__ __launch_bounds__(256) void sa_eqcount_kernel(SegAuction a) {
+  if (a.any_miss && !*a.any_miss) return;
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
   if (!(f & kLive) || (f & kSingle)) return;
@@ -529,7 +634,9 @@ __global__ __launch_bounds__(256) void sa_eqcount_kernel(SegAuction a) {
   if (threadIdx.x < nw) a.eqcnt[(int64_t)(w0 + threadIdx.x) * a.total_chunks + blockIdx.x] = c[threadIdx.x];
 }
 
-// exclusive scan of the tie counts over a segment's chunks: one wave per (segment, worker)
+// exclusive scan of the tie counts over a segment's chunks: one wave per (segment, worker); each lane
+// loads kScanPer consecutive chunks' counts at once (one round of load latency per 64 * kScanPer chunks)
+constexpr int kScanPer = 16;
 __global__ __launch_bounds__(256) void sa_eqscan_kernel(SegAuction a) {
   const int64_t hw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (hw >= (int64_t)a.n_multi * a.K) return;
@@ -542,143 +649,60 @@ __global__ __launch_bounds__(256) void sa_eqscan_kernel(SegAuction a) {
   // a worker the guessed pass found (T in last round's bin): its chunk counts of T are entries of the
   // chunk histograms; a missed worker's come from sa_eqcount_kernel
   const bool from_hist = a.chist && !a.miss[hw];
-  const uint16_t* ch = from_hist ? a.chist + (int64_t)w * 256 + (a.sel[((int64_t)s * a.K + w) * 4 + 2] & 255u) : nullptr;
+  const uint16_t* ch = from_hist ? a.chist + (int64_t)w * a.total_chunks * 256 + (a.sel[((int64_t)s * a.K + w) * 4 + 2] & 255u) : nullptr;
+  const int64_t stride = 256;
   uint32_t carry = 0;
-  for (int64_t base = c0; base < c1; base += 64) {
-    const int64_t i = base + lane;
-    const uint32_t v = i < c1 ? (from_hist ? (uint32_t)ch[i * a.K * 256] : e[i]) : 0;
-    uint32_t x = v;
+  for (int64_t base = c0; base < c1; base += 64 * kScanPer) {
+    const int64_t i0 = base + (int64_t)lane * kScanPer;
+    uint32_t v[kScanPer];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int q = 0; q < kScanPer; ++q) {
+      const int64_t i = min(i0 + q, c1 - 1);
+      v[q] = i0 + q < c1 ? (from_hist ? (uint32_t)ch[i * stride] : e[i]) : 0u;
+      tot += v[q];
+    }
+    uint32_t x = tot;  // inclusive scan of the lanes' totals
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y = (uint32_t)__shfl_up((int)x, o);
       if (lane >= o) x += y;
     }
-    if (i < c1) e[i] = carry + x - v;
+    uint32_t run = carry + x - tot;
+#pragma unroll
+    for (int q = 0; q < kScanPer; ++q) {
+      if (i0 + q < c1) e[i0 + q] = run;
+      run += v[q];
+    }
     carry += (uint32_t)__shfl((int)x, 63);
   }
   if (lane == 0) a.eqtot[(int64_t)s * a.K + w] = carry;
 }
 
-// ---- bids: one packed {fp16 bid, ~worker} atomicMax per job and block ----
-// Phase A settles every value that does not need its tie rank (above T, below T, the retention and
-// leftover overrides) in one pass in fp16 and records each wave's ballot of the values equal to T.
-// Phase B visits only the (job slice, worker) pairs where some lane holds an equal value whose bid
-// depends on its rank among the segment's equal values in job order.
-template <bool VEC>
-__global__ __launch_bounds__(256) void sa_bid_kernel(SegAuction a) {
-  const int counter = *a.round_dev;
-  const ChunkInfo ci = chunk_info(a, blockIdx.x);
-  const uint8_t f = a.flag[ci.s];
-  if (!(f & kLive)) return;
-  __shared__ unsigned long long eqm[kJPT][kKG][4];  // per (job slice, worker, wave): values equal to T
-  const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
-  const int64_t sw0 = (int64_t)ci.s * a.K + w0;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint16_t eps = a.eps[ci.s];
-  const _Float16 epsh = __builtin_bit_cast(_Float16, eps);
-  _Float16 vT[kKG];
-  uint32_t need[kKG], off[kKG];
-  for (int g = 0; g < kKG; ++g) {
-    vT[g] = __builtin_bit_cast(_Float16, g < nw ? okey_inv(a.sel[(sw0 + g) * 4 + 2]) : (uint16_t)0);
-    need[g] = g < nw ? a.sel[(sw0 + g) * 4 + 3] : 0;
-    off[g] = (g < nw && !(f & kSingle)) ? a.eqcnt[(int64_t)(w0 + g) * a.total_chunks + blockIdx.x] : 0;
-    if (g < nw && a.rank_off) off[g] += a.rank_off[w0 + g];
-  }
-  const bool retain = counter < 100;                 // retention bid of the previous winner
-  const bool leftover = counter > 1000 && w0 == 0;   // leftovers go to worker 0
-  uint32_t best[kJPT] = {};
-  uint64_t defer = 0;  // bit t * kKG + g: an equal value whose bid depends on its tie rank
-  ChunkScores cs;
-  load_chunk<VEC>(a, ci, w0, cs);
-  (&eqm[0][0][0])[threadIdx.x] = 0;  // kJPT * kKG * 4 == 256 slots
-  __syncthreads();
-  bool nob[kJPT];
+// ---- resolve one chunk: winners, costs and the count of jobs with a bidder; every load issued before any
+// store.  (A bid kernel whose last block per chunk resolved it measured 17x slower: the cross-block
+// handoff needs device-scope fences, an L2 writeback per block on the XCD-split L2.) ----
+__device__ __forceinline__ void resolve_chunk(const SegAuction& a, const ChunkInfo& ci, int32_t* __restrict__ out) {
+  uint32_t k[kJPT];
+  uint16_t c[kJPT];
 #pragma unroll
   for (int t = 0; t < kJPT; ++t) {
-    const int64_t jj = t * 256 + threadIdx.x;
-    (void)jj;
-    nob[t] = leftover && job_of<VEC>(t) < ci.nj && a.nobid[ci.j0 + job_of<VEC>(t)];
+    const int64_t j = ci.j0 + min((int64_t)(t * 256 + threadIdx.x), ci.nj - 1);
+    k[t] = a.key[j];
+    c[t] = a.cost[j];
   }
-#pragma unroll
-  for (int t = 0; t < kJPT; ++t) {
-    const bool live = job_of<VEC>(t) < ci.nj;
-    const int32_t hbj = live ? cs.hb[t] : -1;
-#pragma unroll
-    for (int g = 0; g < kKG; ++g) {
-      if (g >= nw) continue;
-      const int w = w0 + g;
-      const _Float16 x = value_h(w, cs.v[t][g], hbj, cs.c[t]);
-      // about 1/K of the values reach T: a wave whose lanes are all below it and under no override
-      // has nothing to bid or to count (its eqm slot stays zero)
-      if (!__ballot(live && (x >= vT[g] || (retain && hbj == w) || (g == 0 && nob[t])))) continue;
-      const bool gt = live && x > vT[g];
-      const bool eq = live && x == vT[g];
-      const unsigned long long m = __ballot(eq);
-      if (lane == 0 && m) eqm[t][g][wv] = m;
-      uint32_t bid = gt ? (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)((_Float16)(x - vT[g]) + epsh)) : 0u;
-      if ((retain && hbj == w) || (nob[t] && g == 0)) bid = eps;
-      else if (eq) defer |= 1ull << (t * kKG + g);
-      if (bid) best[t] = max(best[t], (bid << 16) | (0xFFFFu - (uint32_t)w));
-    }
-  }
-  __syncthreads();
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  const uint64_t slice = 0x0001000100010001ull;  // bit t * kKG of every job slice t
-#pragma unroll
-  for (int g = 0; g < kKG; ++g) {
-    if (g >= nw || !__ballot((defer & (slice << g)) != 0)) continue;
-    const uint32_t wbid = ((uint32_t)eps << 16) | (0xFFFFu - (uint32_t)(w0 + g));
-    if (VEC) {
-      // job order: earlier waves, then lower lanes (all four slices), then this lane's earlier slices
-      uint32_t before = off[g], own = 0;
-#pragma unroll
-      for (int t = 0; t < kJPT; ++t) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const unsigned long long m = eqm[t][g][q];
-          before += q < wv ? (uint32_t)__popcll(m) : q == wv ? (uint32_t)__popcll(m & lt) : 0u;
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < kJPT; ++t) {
-        if (((defer >> (t * kKG + g)) & 1ull) && before + own < need[g]) best[t] = max(best[t], wbid);
-        own += (uint32_t)((eqm[t][g][wv] >> lane) & 1ull);
-      }
-      continue;
-    }
-    uint32_t run = off[g];
-#pragma unroll
-    for (int t = 0; t < kJPT; ++t) {
-      const unsigned long long m0 = eqm[t][g][0], m1 = eqm[t][g][1], m2 = eqm[t][g][2], m3 = eqm[t][g][3];
-      const uint32_t c0 = __popcll(m0), c1 = __popcll(m1), c2 = __popcll(m2);
-      if ((defer >> (t * kKG + g)) & 1ull) {
-        const unsigned long long mw = wv == 0 ? m0 : wv == 1 ? m1 : wv == 2 ? m2 : m3;
-        const uint32_t below = wv == 0 ? 0 : wv == 1 ? c0 : wv == 2 ? c0 + c1 : c0 + c1 + c2;
-        if (run + below + (uint32_t)__popcll(mw & lt) < need[g]) best[t] = max(best[t], wbid);
-      }
-      run += c0 + c1 + c2 + (uint32_t)__popcll(m3);
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < kJPT; ++t)
-    if (best[t]) atomicMax(&a.key[ci.j0 + job_of<VEC>(t)], best[t]);
-}
-
-// ---- resolve: per job of the live segments, one block per chunk ----
-__global__ __launch_bounds__(256) void sa_resolve_kernel(SegAuction a, int32_t* __restrict__ out) {
-  const ChunkInfo ci = chunk_info(a, blockIdx.x);
-  if (!(a.flag[ci.s] & kLive)) return;
   uint32_t cnt = 0;
-  for (int64_t t = threadIdx.x; t < ci.nj; t += 256) {
-    const int64_t j = ci.j0 + t;
-    const uint32_t k = a.key[j];
+#pragma unroll
+  for (int t = 0; t < kJPT; ++t) {
+    if (t * 256 + (int64_t)threadIdx.x >= ci.nj) break;
+    const int64_t j = ci.j0 + t * 256 + threadIdx.x;
     a.key[j] = 0;
-    if (k) {
-      const int32_t w = (int32_t)(0xFFFFu - (k & 0xFFFFu));
-      const uint16_t bid = (uint16_t)(k >> 16);
+    if (k[t]) {
+      const int32_t w = (int32_t)(0xFFFFu - (k[t] & 0xFFFFu));
+      const uint16_t bid = (uint16_t)(k[t] >> 16);
       out[j] = w;
       a.hb[j] = w;
       a.nobid[j] = 0;
-      a.cost[j] = f2h(h2f(a.cost[j]) + h2f(bid));
+      a.cost[j] = f2h(h2f(c[t]) + h2f(bid));
       ++cnt;
     } else {
       out[j] = -1;
@@ -697,16 +721,202 @@ __global__ __launch_bounds__(256) void sa_resolve_kernel(SegAuction a, int32_t* 
   }
 }
 
-// end of round r: a segment whose every job has a bidder is done after r+1 rounds
-__global__ void sa_round_inc_kernel(SegAuction a) { *a.round_dev += 1; }
+// ---- bids: one packed {fp16 bid, ~worker} atomicMax per job and block ----
+// A worker bids on its values above T and on the first `need` of its values equal to T in job order.  The
+// tie offsets (eqcnt: equal values in the segment's earlier chunks; eqtot: the segment's total) put each
+// chunk of a worker in one of three cases: no equal value bids (need <= offset), every equal value bids
+// (need >= offset + the chunk's count: the test becomes x >= T, i.e. x > below(T), whose bid (x - T) + eps
+// is eps at equality, the deferred bid's key), or the chunk straddles the boundary and its equal values
+// need their ranks: one chunk per worker and round of a wide segment, every chunk of a one-chunk segment.
+// Only blocks with a straddling worker re-read their chunk (L2) for its equal values and rank them (phase B).
+// Phase A is branch-free per value (RET: the retention rounds, where the previous winner bids eps): a bid
+// key or a bid-less key (< 2^16) is max-ed into each job slice.  A ranked equal value of an overridden job
+// (retention / leftover) is harmless: its phase-B bid is the same eps key.
+template <bool RET>
+__device__ __forceinline__ void bid_values(const ChunkScores& cs, const LaneJobs& lj, const bool (&nob)[kJPT],
+                                           const _Float16 (&vT)[kKG], const _Float16 (&vC)[kKG], int w0,
+                                           _Float16 epsh, uint32_t (&best)[kJPT]) {
+  const uint32_t eps = __builtin_bit_cast(uint16_t, epsh);
+#pragma unroll
+  for (int t = 0; t < kJPT; ++t) {
+#pragma unroll
+    for (int g = 0; g < kKG; ++g) {
+      const int w = w0 + g;
+      const bool own = lj.hb[t] == w;
+      const _Float16 x = __builtin_bit_cast(_Float16, cs.v[t][g]) - (own ? (_Float16)-0.0f : lj.c[t]);
+      uint32_t bid = x > vC[g] ? (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)((_Float16)(x - vT[g]) + epsh)) : 0u;
+      if (RET) bid = own ? eps : bid;
+      if (g == 0) bid = nob[t] ? eps : bid;
+      best[t] = max(best[t], (bid << 16) | (0xFFFFu - (uint32_t)w));
+    }
+  }
+}
 
+// the straddling workers' values equal to T: bit (t & 1) * kKG + g of eqs[t >> 1]
+__device__ __forceinline__ void equal_values(const ChunkScores& cs, const LaneJobs& lj, const _Float16 (&vT)[kKG],
+                                             uint32_t straddle, int w0, uint32_t (&eqs)[2]) {
+#pragma unroll
+  for (int g = 0; g < kKG; ++g) {
+    if (!((straddle >> g) & 1u)) continue;
+#pragma unroll
+    for (int t = 0; t < kJPT; ++t) {
+      const _Float16 x = __builtin_bit_cast(_Float16, cs.v[t][g]) - (lj.hb[t] == w0 + g ? (_Float16)-0.0f : lj.c[t]);
+      eqs[t >> 1] |= x == vT[g] ? 1u << ((t & 1) * kKG + g) : 0u;
+    }
+  }
+}
+
+// the largest fp16 value below the one of key k (k of a finite value; +0's predecessor is -min_subnormal)
+__device__ __forceinline__ _Float16 value_below(uint32_t k) {
+  const uint32_t p = k - 1u == 0x7FFFu ? 0x7FFEu : k - 1u;
+  return __builtin_bit_cast(_Float16, okey_inv(p));
+}
+
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// RQ_BID_WAVES: occupancy floor for the bid kernel (0 = the compiler's choice: 103 VGPRs, 4 waves/SIMD, 1.6x
+// slower at K=128 x 1M; 5 keeps both forms spill-free, A/B in profiles/r3_auction_ab_waves.txt)
+#ifndef RQ_BID_WAVES
+#define RQ_BID_WAVES 5
+#endif
+#if RQ_BID_WAVES
+#define RQ_BID_ATTR __attribute__((amdgpu_waves_per_eu(RQ_BID_WAVES)))
+#else
+#define RQ_BID_ATTR
+#endif
+template <bool VEC>
+__global__ __launch_bounds__(256) RQ_BID_ATTR void sa_bid_kernel(SegAuction a) {
+  const int counter = *a.round_dev;
+  const ChunkInfo ci = chunk_info(a, blockIdx.x);
+  const uint8_t f = a.flag[ci.s];
+  if (!(f & kLive)) return;
+  __shared__ uint4 eqc[kKG][4];  // per (worker, wave): values equal to T in each job slice
+  __shared__ uint32_t gneed[kKG], goff[kKG];
+  const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
+  const int64_t sw0 = (int64_t)ci.s * a.K + w0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint16_t eps = a.eps[ci.s];
+  const _Float16 epsh = __builtin_bit_cast(_Float16, eps);
+  const bool single = f & kSingle;
+  const int64_t c = blockIdx.x, c_last = a.chunk_off[ci.s + 1] - 1;
+  _Float16 vT[kKG], vC[kKG];  // T and the comparison bound; NaN for workers past K (nothing bids)
+  uint32_t need[kKG], off[kKG];
+  uint32_t straddle = 0;
+  for (int g = 0; g < kKG; ++g) {
+    vT[g] = vC[g] = __builtin_bit_cast(_Float16, (uint16_t)0x7E00u);
+    need[g] = off[g] = 0;
+    if (g >= nw) continue;
+    const uint32_t kT = a.sel[(sw0 + g) * 4 + 2];
+    need[g] = a.sel[(sw0 + g) * 4 + 3];
+    vT[g] = vC[g] = __builtin_bit_cast(_Float16, okey_inv(kT));
+    if (single) {  // need < the segment's equal values: all-or-none only at need == 0
+      if (need[g]) straddle |= 1u << g;
+      continue;
+    }
+    const uint32_t* e = a.eqcnt + (int64_t)(w0 + g) * a.total_chunks;
+    const uint32_t lo = e[c], n = (c < c_last ? e[c + 1] : a.eqtot[sw0 + g]) - lo;
+    off[g] = lo + (a.rank_off ? a.rank_off[w0 + g] : 0u);
+    if (need[g] >= off[g] + n) vC[g] = value_below(kT);
+    else if (need[g] > off[g]) straddle |= 1u << g;
+  }
+  const bool leftover = counter > 1000 && w0 == 0;   // leftovers go to worker 0
+  ChunkScores cs;
+  load_chunk<VEC>(a, ci, w0, cs);
+  const LaneJobs lj = lane_jobs<VEC>(ci, cs);
+  bool nob[kJPT];
+#pragma unroll
+  for (int t = 0; t < kJPT; ++t) nob[t] = leftover && job_of<VEC>(t) < ci.nj && a.nobid[ci.j0 + job_of<VEC>(t)];
+  uint32_t best[kJPT] = {};
+  if (counter < 100) bid_values<true>(cs, lj, nob, vT, vC, w0, epsh, best);
+  else bid_values<false>(cs, lj, nob, vT, vC, w0, epsh, best);
+  if (straddle) {  // block-uniform: phase B's barrier is reached by every wave
+    ChunkScores cr;  // the chunk again (L2-resident), so phase A keeps no values alive for this rare path
+    load_chunk<VEC>(a, ci, w0, cr);
+    uint32_t eqs[2] = {};
+    equal_values(cr, lj, vT, straddle, w0, eqs);
+    // straddling workers with an equal value in this wave (OR over the lanes); loops over worker bits
+    // with the worker's need and offset from LDS keep the rare path's registers out of phase A's budget
+    uint32_t any = eqs[0] | eqs[1];
+    for (int o = 32; o > 0; o >>= 1) any |= (uint32_t)__shfl_xor((int)any, o);
+    const uint32_t weq = (uint32_t)__builtin_amdgcn_readfirstlane((int)((any | (any >> kKG)) & straddle));
+    if (threadIdx.x == 0) {
+      for (int g = 0; g < kKG; ++g) {
+        gneed[g] = need[g];
+        goff[g] = off[g];
+      }
+    }
+    for (uint32_t m = straddle; m; m &= m - 1u) {
+      const int g = __builtin_ctz(m);
+      uint32_t n[kJPT] = {};
+      if ((weq >> g) & 1u) {
+#pragma unroll
+        for (int t = 0; t < kJPT; ++t) n[t] = (uint32_t)__popcll(__ballot((eqs[t >> 1] >> ((t & 1) * kKG + g)) & 1u));
+      }
+      if (lane == 0) eqc[g][wv] = make_uint4(n[0], n[1], n[2], n[3]);
+    }
+    __syncthreads();
+    for (uint32_t m = weq; m; m &= m - 1u) {
+      const int g = __builtin_ctz(m);
+      const uint32_t wbid = ((uint32_t)eps << 16) | (0xFFFFu - (uint32_t)(w0 + g));
+      const uint32_t ng = gneed[g];
+      const uint4 q0 = eqc[g][0], q1 = eqc[g][1], q2 = eqc[g][2], q3 = eqc[g][3];
+      const uint32_t n0[kJPT] = {q0.x, q0.y, q0.z, q0.w}, n1[kJPT] = {q1.x, q1.y, q1.z, q1.w},
+                     n2[kJPT] = {q2.x, q2.y, q2.z, q2.w}, n3[kJPT] = {q3.x, q3.y, q3.z, q3.w};
+      bool e[kJPT];
+#pragma unroll
+      for (int t = 0; t < kJPT; ++t) e[t] = (eqs[t >> 1] >> ((t & 1) * kKG + g)) & 1u;
+      if (VEC) {
+        // job order: earlier waves (all slices), lower lanes (all slices), this lane's earlier slices
+        uint32_t before = goff[g];
+#pragma unroll
+        for (int t = 0; t < kJPT; ++t)
+          before += (wv > 0 ? n0[t] : 0u) + (wv > 1 ? n1[t] : 0u) + (wv > 2 ? n2[t] : 0u) + lanes_below(__ballot(e[t]));
+#pragma unroll
+        for (int t = 0; t < kJPT; ++t) {
+          if (e[t] && before < ng) best[t] = max(best[t], wbid);
+          before += e[t];
+        }
+      } else {
+        // job order: slice-major, then waves, then lanes
+        uint32_t run = goff[g];
+#pragma unroll
+        for (int t = 0; t < kJPT; ++t) {
+          const uint32_t r = run + (wv > 0 ? n0[t] : 0u) + (wv > 1 ? n1[t] : 0u) + (wv > 2 ? n2[t] : 0u) +
+                             lanes_below(__ballot(e[t]));
+          if (e[t] && r < ng) best[t] = max(best[t], wbid);
+          run += n0[t] + n1[t] + n2[t] + n3[t];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < kJPT; ++t)
+    if (best[t] >> 16) atomicMax(&a.key[ci.j0 + job_of<VEC>(t)], best[t]);
+}
+
+// ---- resolve: per job of the live segments, one block per chunk ----
+__global__ __launch_bounds__(256) void sa_resolve_kernel(SegAuction a, int32_t* __restrict__ out) {
+  const ChunkInfo ci = chunk_info(a, blockIdx.x);
+  if (!(a.flag[ci.s] & kLive)) return;
+  resolve_chunk(a, ci, out);
+}
+
+// end of a round: a segment whose every job has a bidder is done (it was live from round 0, so its
+// round count is the rounds it took); the round number advances for the next round's bids (nothing in
+// this kernel reads it)
 __global__ __launch_bounds__(256) void sa_round_end_kernel(SegAuction a, int count) {
-  const int round = *a.round_dev;
   const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s == 0) {
+    *a.round_dev += 1;
+    if (a.any_miss) *a.any_miss = 0;  // for the next round's select_guess (a store at the top of the guessed
+                                      // pass would turn its uniform loads into vector loads)
+  }
   uint32_t live = 0;
   if (s < a.S && (a.flag[s] & kLive)) {
     const int64_t n_s = a.n_glob ? a.n_glob : a.seg_off[s + 1] - a.seg_off[s];
-    a.rounds[s] = round + 1;
+    a.rounds[s] += 1;
     if ((int64_t)a.have[s] == n_s) a.flag[s] &= ~kLive;
     else live = 1;
     a.have[s] = 0;
@@ -779,6 +989,7 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.above = guess ? c.take<uint32_t>((int64_t)a.n_multi * K * kAbovePad) : nullptr;
   a.miss = guess ? c.take<uint8_t>((int64_t)a.n_multi * K) : nullptr;
   a.chist = guess && a.n_multi > 0 ? c.take<uint16_t>(total_chunks * K * 256) : nullptr;
+  a.any_miss = guess ? c.take<uint32_t>(1) : nullptr;
 }
 
 }  // namespace
@@ -866,7 +1077,8 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   const size_t mk = (size_t)n_multi * n_workers;
   if (n_multi > 0 && (hipMemsetAsync(a.hist, 0, mk * 256 * 4, st) != hipSuccess ||
                       hipMemsetAsync(a.above, 0, mk * kAbovePad * 4, st) != hipSuccess ||
-                      hipMemsetAsync(a.miss, 1, mk, st) != hipSuccess))
+                      hipMemsetAsync(a.miss, 1, mk, st) != hipSuccess ||
+                      hipMemsetAsync(a.any_miss, 0, 4, st) != hipSuccess))
     return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   hipLaunchKernelGGL(sa_job_init_kernel, dim3(grid_cap(cdiv(n_jobs, 256), 8192)), dim3(256), 0, st, a, n_jobs);
   const dim3 gcw((unsigned)total_chunks, (unsigned)cdiv(n_workers, kKG));
@@ -883,8 +1095,8 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   constexpr int kPoll = 8;
   auto launch_round = [&](hipStream_t q, bool count) {
     if (n_multi > 0) {
-      if (vec) hipLaunchKernelGGL((sa_hist_kernel<2, true>), gcw, dim3(256), 0, q, a);
-      else hipLaunchKernelGGL((sa_hist_kernel<2, false>), gcw, dim3(256), 0, q, a);
+      if (vec) hipLaunchKernelGGL((sa_guess_hist_kernel<true>), gcw, dim3(256), 0, q, a);
+      else hipLaunchKernelGGL((sa_guess_hist_kernel<false>), gcw, dim3(256), 0, q, a);
       hipLaunchKernelGGL(sa_select_guess_kernel, dim3(gmw), dim3(256), 0, q, a);
       // the two-pass selection for the workers the guessed pass missed (every block exits at once
       // when none of its workers missed)
@@ -903,7 +1115,6 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     else hipLaunchKernelGGL((sa_bid_kernel<false>), gcw, dim3(256), 0, q, a);
     hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, q, a, out_assign);
     hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
-    hipLaunchKernelGGL(sa_round_inc_kernel, dim3(1), dim3(1), 0, q, a);
   };
   // capture one block on a private stream (the caller's may be the null stream, which cannot capture)
   hipGraphExec_t exec = nullptr;
@@ -1137,7 +1348,6 @@ int rqsid_dauction_end_round(const uint16_t* scores, int32_t n_workers, int64_t 
   int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
   if (rc) return rc;
   hipLaunchKernelGGL(sa_round_end_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, a, 0);
-  hipLaunchKernelGGL(sa_round_inc_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, a);
   return check_launch("dauction_end_round");
 }
 

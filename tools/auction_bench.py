@@ -18,18 +18,36 @@ def main():
     ap.add_argument("--jobs", type=int, default=100000)
     ap.add_argument("--workers", type=int, default=1280)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--segments", type=int, default=0,
+                    help="S > 0: S equal segments, each its own K-worker auction (ops.seg_auction, the lockstep "
+                         "sub-fits' form)")
     a = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(1)
     x = torch.randn(a.jobs, 512, device="cuda", generator=g)
-    c = torch.randn(a.workers, 512, device="cuda", generator=g)
-    w = ops.auction_scores(x, c, half=True)
+    if a.segments:
+        import numpy as np
+        sizes = np.full(a.segments, a.jobs // a.segments)
+        sizes[: a.jobs % a.segments] += 1
+        lay = ops.SegmentLayout(sizes, torch.device("cuda"))
+        c = torch.randn(a.segments * a.workers, 512, device="cuda", generator=g)
+        w = ops.seg_auction_scores(x, c, a.workers, lay)
+
+        def run():
+            _, rr = ops.seg_auction(w, a.workers, lay)
+            return int(rr.max().item())
+    else:
+        c = torch.randn(a.workers, 512, device="cuda", generator=g)
+        w = ops.auction_scores(x, c, half=True)
+
+        def run():
+            return ops.auction(w)[1]
     for r in range(a.reps):
         torch.cuda.synchronize()
         t = time.time()
-        _, rounds = ops.auction(w)
+        rounds = run()
         torch.cuda.synchronize()
         dt = time.time() - t
-        print(json.dumps({"jobs": a.jobs, "workers": a.workers, "rounds": rounds, "s": round(dt, 3),
+        print(json.dumps({"jobs": a.jobs, "workers": a.workers, "segments": a.segments, "rounds": rounds, "s": round(dt, 3),
                           "ms_per_round": round(1e3 * dt / max(rounds, 1), 4),
                           "W_GB": round(2 * a.jobs * a.workers / 1e9, 3)}), flush=True)
 
