@@ -507,6 +507,56 @@ __global__ __launch_bounds__(256) void sa_select_kernel(SegAuction a) {
   for (int i = lane; i < 256; i += 64) h[i] = 0;  // ready for the next histogram
 }
 
+// Exclusive scan of one worker's per-chunk tie counts over its segment's chunks (one wave), into the eqcnt
+// offsets and the segment total eqtot.  The counts come from the guessed pass's chunk histograms (ch: the
+// worker's run at slot T & 255; a hit worker, from select_guess) or from sa_eqcount_kernel (eqcnt itself).
+// Each lane loads kScanPer consecutive chunks' counts at once: one round of load latency per 64 * kScanPer
+// chunks.
+constexpr int kScanPer = 16;
+__device__ __forceinline__ void scan_ties(const SegAuction& a, int s, int w, const uint16_t* __restrict__ ch) {
+  const int lane = threadIdx.x & 63;
+  uint32_t* e = a.eqcnt + (int64_t)w * a.total_chunks;
+  const int64_t c0 = a.chunk_off[s], c1 = a.chunk_off[s + 1];
+  uint32_t carry = 0;
+  for (int64_t base = c0; base < c1; base += 64 * kScanPer) {
+    const int64_t i0 = base + (int64_t)lane * kScanPer;
+    uint32_t v[kScanPer];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int q = 0; q < kScanPer; ++q) {
+      const int64_t i = min(i0 + q, c1 - 1);
+      v[q] = i0 + q < c1 ? (ch ? (uint32_t)ch[i * 256] : e[i]) : 0u;
+      tot += v[q];
+    }
+    uint32_t x = tot;  // inclusive scan of the lanes' totals
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+      if (lane >= o) x += y;
+    }
+    uint32_t run = carry + x - tot;
+#pragma unroll
+    for (int q = 0; q < kScanPer; ++q) {
+      if (i0 + q < c1) e[i0 + q] = run;
+      run += v[q];
+    }
+    carry += (uint32_t)__shfl((int)x, 63);
+  }
+  if (lane == 0) a.eqtot[(int64_t)s * a.K + w] = carry;
+}
+
+// the tie-count scan of the workers the guessed pass missed (one wave per (segment, worker)), or of every
+// worker in the row-sharded mode
+__global__ __launch_bounds__(256) void sa_eqscan_kernel(SegAuction a) {
+  if (a.any_miss && !*a.any_miss) return;
+  const int64_t hw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (hw >= (int64_t)a.n_multi * a.K) return;
+  const int s = a.mseg[hw / a.K];
+  const int w = (int)(hw % a.K);
+  if (!(a.flag[s] & kLive)) return;
+  if (a.chist && !a.miss[hw]) return;  // scanned by select_guess
+  scan_ties(a, s, w, nullptr);
+}
+
 // the guessed pass's selection: exact when the (jpw+1)-th largest value lies in last round's bin b1
 // (values above b1 < rank <= values at or above b1); otherwise a miss for the two-pass selection
 __global__ __launch_bounds__(256) void sa_select_guess_kernel(SegAuction a) {
@@ -537,6 +587,8 @@ __global__ __launch_bounds__(256) void sa_select_guess_kernel(SegAuction a) {
     a.above[hw * kAbovePad] = 0;
   }
   for (int i = lane; i < 256; i += 64) h[i] = 0;
+  // a hit worker's chunk counts of T are its chunk histograms' slot T & 255 = b
+  if (hit) scan_ties(a, s, w, a.chist + (int64_t)w * a.total_chunks * 256 + b);
 }
 
 // one-chunk segments: both histogram passes and both selections inside the block; the chunk offset of
@@ -604,11 +656,12 @@ __global__ __launch_bounds__(256) void sa_eqcount_kernel(SegAuction a) {
   __shared__ uint32_t c[kKG];
   const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
   const int64_t sw0 = (int64_t)ci.s * a.K + w0;
-  if (a.chist) {  // hit workers take their counts from the guessed pass's chunk histograms (eqscan)
+  uint32_t part = (1u << nw) - 1u;  // workers whose counts this pass produces
+  if (a.chist) {  // hit workers' counts come from the guessed pass's chunk histograms (select_guess)
     const int64_t hw0 = (int64_t)a.hidx[ci.s] * a.K + w0;
-    bool any = false;
-    for (int g = 0; g < nw; ++g) any |= a.miss[hw0 + g] != 0;
-    if (!any) return;
+    part = 0;
+    for (int g = 0; g < nw; ++g) part |= (uint32_t)(a.miss[hw0 + g] != 0) << g;
+    if (!part) return;
   }
   if (threadIdx.x < kKG) c[threadIdx.x] = 0;
   __syncthreads();
@@ -631,51 +684,8 @@ __global__ __launch_bounds__(256) void sa_eqcount_kernel(SegAuction a) {
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(&c[g], v);
   }
   __syncthreads();
-  if (threadIdx.x < nw) a.eqcnt[(int64_t)(w0 + threadIdx.x) * a.total_chunks + blockIdx.x] = c[threadIdx.x];
-}
-
-// exclusive scan of the tie counts over a segment's chunks: one wave per (segment, worker); each lane
-// loads kScanPer consecutive chunks' counts at once (one round of load latency per 64 * kScanPer chunks)
-constexpr int kScanPer = 16;
-__global__ __launch_bounds__(256) void sa_eqscan_kernel(SegAuction a) {
-  const int64_t hw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (hw >= (int64_t)a.n_multi * a.K) return;
-  const int s = a.mseg[hw / a.K];
-  const int w = (int)(hw % a.K);
-  if (!(a.flag[s] & kLive)) return;
-  const int lane = threadIdx.x & 63;
-  uint32_t* e = a.eqcnt + (int64_t)w * a.total_chunks;
-  const int64_t c0 = a.chunk_off[s], c1 = a.chunk_off[s + 1];
-  // a worker the guessed pass found (T in last round's bin): its chunk counts of T are entries of the
-  // chunk histograms; a missed worker's come from sa_eqcount_kernel
-  const bool from_hist = a.chist && !a.miss[hw];
-  const uint16_t* ch = from_hist ? a.chist + (int64_t)w * a.total_chunks * 256 + (a.sel[((int64_t)s * a.K + w) * 4 + 2] & 255u) : nullptr;
-  const int64_t stride = 256;
-  uint32_t carry = 0;
-  for (int64_t base = c0; base < c1; base += 64 * kScanPer) {
-    const int64_t i0 = base + (int64_t)lane * kScanPer;
-    uint32_t v[kScanPer];
-    uint32_t tot = 0;
-#pragma unroll
-    for (int q = 0; q < kScanPer; ++q) {
-      const int64_t i = min(i0 + q, c1 - 1);
-      v[q] = i0 + q < c1 ? (from_hist ? (uint32_t)ch[i * stride] : e[i]) : 0u;
-      tot += v[q];
-    }
-    uint32_t x = tot;  // inclusive scan of the lanes' totals
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-      if (lane >= o) x += y;
-    }
-    uint32_t run = carry + x - tot;
-#pragma unroll
-    for (int q = 0; q < kScanPer; ++q) {
-      if (i0 + q < c1) e[i0 + q] = run;
-      run += v[q];
-    }
-    carry += (uint32_t)__shfl((int)x, 63);
-  }
-  if (lane == 0) a.eqtot[(int64_t)s * a.K + w] = carry;
+  if (threadIdx.x < nw && ((part >> threadIdx.x) & 1u))
+    a.eqcnt[(int64_t)(w0 + threadIdx.x) * a.total_chunks + blockIdx.x] = c[threadIdx.x];
 }
 
 // ---- resolve one chunk: winners, costs and the count of jobs with a bidder; every load issued before any
