@@ -385,40 +385,60 @@ __device__ __forceinline__ _Float16 lane_value(int w, uint16_t v, int32_t hbj, _
   return __builtin_bit_cast(_Float16, v) - (hbj == w ? (_Float16)-0.0f : c);
 }
 
-// The guessed pass: per worker, the low-byte histogram of its values in last round's high-byte bin b1
-// (sel[0]) and the count of values above that bin, in one sweep with no ballots and no branches per value
-// other than the LDS atomic: d = okey(x) - (b1 << 8) is the bin slot (0..255), >= 256 above the bin (slot
-// 256), negative below.  Both the values in b1 and those above it are about 1/K of a worker's values, so
-// the predicated atomic is rare.  d comes from x's raw bits in one operation, by the sign of the bin's
-// values (uniform per worker): x = v + (0 - c) is never -0 (a round-to-nearest sum is -0 only when both
-// addends are), so okey(x) = bits | 0x8000 for x >= +0 and 0xFFFF - bits for x < 0, and
-//   a bin of values >= +0 (b1 >= 0x80): d = sext16(bits) + 0x8000 - base (every x < 0 lands below),
-//   a bin of values < 0:                d = 0xFFFF - base - bits (every x >= +0 lands above).
-// A lane past the chunk's end takes the cost +inf (x = -inf: below every bin of a finite threshold); a
-// threshold of -inf (b1 < 4) takes explicit dead offsets (DEAD).
-constexpr int kGStride = 260;  // LDS words per worker: 256 low-byte slots + the above count, padded to 16 B
+// The guessed pass: per worker, the histogram of its values' keys in a 256-key window around last round's
+// threshold (window_base) and the count of keys above the window, in one sweep with no ballots and no
+// branches per value other than the LDS atomic: d = okey(x) - base is the window slot (0..255), >= 256
+// above the window (slot 256), negative below.  Both the values in the window and those above it are
+// about 1/K of a worker's values, so the predicated atomic is rare.  d comes from x's raw bits in one
+// operation, by the sign of the window's keys (uniform per worker): x = v + (0 - c) is never -0 (a
+// round-to-nearest sum is -0 only when both addends are), so okey(x) = bits | 0x8000 for x >= +0 and
+// 0xFFFF - bits for x < 0, and
+//   a window of keys >= 0x8000 (values >= +0): d = sext16(bits) + 0x8000 - base (every x < 0 lands below),
+//   a window of negative values:               d = 0xFFFF - base - bits (every x >= +0 lands above).
+// A lane past the chunk's end takes the cost +inf (x = -inf: below every window of finite keys); a window
+// that reaches -inf's key (base < 0x400) takes explicit dead offsets (DEAD).
+constexpr int kGStride = 260;  // LDS words per worker: 256 window slots + the above count, padded to 16 B
 
-template <bool NEG, bool DEAD>
+// The guessed window: 256 consecutive keys centred on last round's threshold T (sel[2]), kept on one
+// side of the sign boundary (0x8000) so that d = okey(x) - base is one operation on x's bits.  A
+// threshold that moves less than ~128 keys stays inside it (a window aligned to T's high byte missed
+// whenever T crossed a byte boundary).
+template <int SH = 0>
+__device__ __forceinline__ int32_t window_base(uint32_t T) {
+  constexpr int32_t span = 256 << SH;
+  const int32_t t = (int32_t)(T & 0xFFFFu) - span / 2;
+  return T >= 0x8000u ? min(max(t, 0x8000), 0x10000 - span) : min(max(t, 0), 0x8000 - span);
+}
+
+// SH > 0 (one-chunk segments): a coarse window of 256 slots of 2^SH keys; FINE: the second pass, counting
+// the keys inside the selected coarse slot csl (2^SH fine slots, stride hs per worker)
+template <bool NEG, bool DEAD, int SH, bool FINE>
 __device__ __forceinline__ void guess_worker(const uint16_t (&v)[kJPT], const LaneJobs& lj, const _Float16 (&nc)[kJPT],
-                                             int w, int32_t addk, uint32_t* __restrict__ hg) {
+                                             int w, int32_t addk, int32_t csl, uint32_t* __restrict__ hg) {
 #pragma unroll
   for (int t = 0; t < kJPT; ++t) {
     const _Float16 x = __builtin_bit_cast(_Float16, v[t]) + (lj.hb[t] == w ? (_Float16)0.0f : nc[t]);
     const uint32_t b = __builtin_bit_cast(uint16_t, x);
     int32_t d = NEG ? addk - (int32_t)b : (int32_t)(int16_t)b + addk;
     if (DEAD) d += lj.dead[t];
-    if (d >= 0) atomicAdd(&hg[min(d, 256)], 1u);
+    if (FINE) {
+      if ((d >> SH) == csl) atomicAdd(&hg[d & ((1 << SH) - 1)], 1u);
+    } else {
+      if (d >= 0) atomicAdd(&hg[min(d >> SH, 256)], 1u);
+    }
   }
 }
 
-template <bool DEAD>
+template <bool DEAD, int SH = 0, bool FINE = false>
 __device__ __forceinline__ void guess_values(const ChunkScores& cs, const LaneJobs& lj, const _Float16 (&nc)[kJPT],
-                                             const int32_t (&addk)[kKG], uint32_t negbin, int w0, uint32_t* h) {
+                                             const int32_t (&addk)[kKG], uint32_t negbin, int w0, uint32_t* h,
+                                             const int32_t* csl = nullptr, int hs = kGStride) {
 #pragma unroll
   for (int g = 0; g < kKG; ++g) {
     const uint16_t v[kJPT] = {cs.v[0][g], cs.v[1][g], cs.v[2][g], cs.v[3][g]};
-    if ((negbin >> g) & 1u) guess_worker<true, DEAD>(v, lj, nc, w0 + g, addk[g], h + g * kGStride);
-    else guess_worker<false, DEAD>(v, lj, nc, w0 + g, addk[g], h + g * kGStride);
+    const int32_t c = FINE ? csl[g] : 0;
+    if ((negbin >> g) & 1u) guess_worker<true, DEAD, SH, FINE>(v, lj, nc, w0 + g, addk[g], c, h + g * hs);
+    else guess_worker<false, DEAD, SH, FINE>(v, lj, nc, w0 + g, addk[g], c, h + g * hs);
   }
 }
 
@@ -440,7 +460,7 @@ __global__ __launch_bounds__(256) void sa_guess_hist_kernel(SegAuction a) {
   for (int g = 0; g < kKG; ++g) {
     addk[g] = -0x20000;
     if (g >= nw) continue;
-    const int32_t base = (int32_t)((a.sel[(sw0 + g) * 4 + 0] & 255u) << 8);
+    const int32_t base = window_base(a.sel[(sw0 + g) * 4 + 2]);
     if (base >= 0x8000) {
       addk[g] = 0x8000 - base;
     } else {
@@ -578,8 +598,9 @@ __global__ __launch_bounds__(256) void sa_select_guess_kernel(SegAuction a) {
   if (hit) wave_select(h, rank - ab, b, above);
   if (lane == 0) {
     if (hit) {
-      sel[0] &= 255u;
-      sel[2] = (sel[0] << 8) | b;
+      const uint32_t T = (uint32_t)window_base(sel[2]) + b;
+      sel[0] = T >> 8;
+      sel[2] = T;
       sel[3] = jpw - (ab + above);
     }
     a.miss[hw] = hit ? 0 : 1;
@@ -591,20 +612,185 @@ __global__ __launch_bounds__(256) void sa_select_guess_kernel(SegAuction a) {
   if (hit) scan_ties(a, s, w, a.chist + (int64_t)w * a.total_chunks * 256 + b);
 }
 
-// one-chunk segments: both histogram passes and both selections inside the block; the chunk offset of
-// the tie ranks is 0
+// sorted (descending) top 4 of 4 keys; top 4 of two sorted lists: the bitonic half-cleaner max(a_i,
+// b_{3-i}) then the 4-element bitonic merge
+__device__ __forceinline__ void cas_desc(uint32_t& x, uint32_t& y) {
+  const uint32_t hi = max(x, y), lo = min(x, y);
+  x = hi;
+  y = lo;
+}
+__device__ __forceinline__ void top4_sort(uint32_t (&k)[4]) {
+  cas_desc(k[0], k[1]);
+  cas_desc(k[2], k[3]);
+  cas_desc(k[0], k[2]);
+  cas_desc(k[1], k[3]);
+  cas_desc(k[1], k[2]);
+}
+__device__ __forceinline__ void top4_merge(uint32_t (&k)[4], const uint32_t (&q)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) k[i] = max(k[i], q[3 - i]);
+  cas_desc(k[0], k[2]);
+  cas_desc(k[1], k[3]);
+  cas_desc(k[0], k[1]);
+  cas_desc(k[2], k[3]);
+}
+
+// one-chunk segments: the selections inside the block; the chunk offset of the tie ranks is 0.  The block
+// holds every value of its workers: the guess is the wide segments' window pass on them (kSmallSh > 0: a
+// coarse window of 256 slots of 2^kSmallSh keys, then a second in-register pass over the keys of the
+// selected slot; measured slower at 3: 0.74 vs 0.55 ms per round of the PROD groups shape, as more values
+// fall inside the window).  A worker whose threshold left the window takes the top-4 merge (jpw < 4, the
+// PROD groups: a worker's threshold there moves by ~100 keys per round as its few top jobs change owners)
+// or both exact histogram passes.
+constexpr int kSmallSh = 0;
 __global__ __launch_bounds__(256) void sa_small_select_kernel(SegAuction a) {
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
   if (!(f & kLive) || !(f & kSingle)) return;
-  __shared__ uint32_t h[kKG][256];
+  __shared__ uint2 lbuf[kKG * 256];  // the histograms, or each lane's sorted top 4 keys per worker (u16 x 4)
+  uint32_t* const h = reinterpret_cast<uint32_t*>(lbuf);
+  static_assert(kKG * kGStride * 4 <= kKG * 256 * 8, "histograms fit the top-4 buffer");
+  constexpr int kFine = 1 << kSmallSh;
+  __shared__ uint32_t hf[kKG][kFine];
+  __shared__ int32_t csl[kKG];
   __shared__ uint32_t b1s[kKG], rk[kKG], ab1[kKG];
+  __shared__ uint32_t missm;
   const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
   const int64_t sw0 = (int64_t)ci.s * a.K + w0;
   const uint32_t jpw = (uint32_t)(ci.n_s / a.K);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < kKG * kGStride / 4; i += 256) reinterpret_cast<uint4*>(h)[i] = make_uint4(0, 0, 0, 0);
+  if (threadIdx.x < kKG * kFine) (&hf[0][0])[threadIdx.x] = 0;
+  if (threadIdx.x == 0) missm = 0;
+  int32_t addk[kKG];
+  uint32_t negbin = 0;
+  bool low = false;
+  for (int g = 0; g < kKG; ++g) {
+    addk[g] = -0x20000;
+    if (g >= nw) continue;
+    const int32_t base = window_base<kSmallSh>(a.sel[(sw0 + g) * 4 + 2]);
+    if (base >= 0x8000) {
+      addk[g] = 0x8000 - base;
+    } else {
+      addk[g] = 0xFFFF - base;
+      negbin |= 1u << g;
+      low |= base < 0x400;
+    }
+  }
+  {
+    ChunkScores cs;
+    load_chunk<false>(a, ci, w0, cs);
+    const LaneJobs lj = lane_jobs<false>(ci, cs);
+    _Float16 nc[kJPT];
+#pragma unroll
+    for (int t = 0; t < kJPT; ++t) nc[t] = lj.dead[t] ? (_Float16)-INFINITY : (_Float16)0.0f - lj.c[t];
+    __syncthreads();
+    if (low) guess_values<true, kSmallSh>(cs, lj, nc, addk, negbin, w0, h);
+    else guess_values<false, kSmallSh>(cs, lj, nc, addk, negbin, w0, h);
+    __syncthreads();
+    // coarse selection: slot c holds the threshold when the window does
+    for (int g = wv; g < kKG; g += 4) {
+      const uint32_t* hg = h + g * kGStride;
+      const uint32_t ab = hg[256], rank = jpw + 1;
+      uint32_t cnt = hg[lane] + hg[lane + 64] + hg[lane + 128] + hg[lane + 192];
+      for (int o = 32; o > 0; o >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, o);
+      const bool hit = g < nw && ab < rank && rank <= ab + cnt;
+      uint32_t c = 0, above = 0;
+      if (hit) wave_select(hg, rank - ab, c, above);
+      if (lane == 0) {
+        csl[g] = hit ? (int32_t)c : 0x7FFFFFFF;  // a missed worker counts nothing in the fine pass
+        rk[g] = rank - ab - above;
+        ab1[g] = ab + above;
+        if (g < nw && !hit) atomicOr(&missm, 1u << g);
+      }
+    }
+    if constexpr (kSmallSh > 0) {
+      __syncthreads();
+      int32_t cs_l[kKG];
+#pragma unroll
+      for (int g = 0; g < kKG; ++g) cs_l[g] = csl[g];
+      if (low) guess_values<true, kSmallSh, true>(cs, lj, nc, addk, negbin, w0, &hf[0][0], cs_l, kFine);
+      else guess_values<false, kSmallSh, true>(cs, lj, nc, addk, negbin, w0, &hf[0][0], cs_l, kFine);
+    }
+  }
+  __syncthreads();
+  {  // fine selection, one thread per hit worker
+    const int g = threadIdx.x;
+    if (g < nw && !((missm >> g) & 1u)) {
+      uint32_t acc = 0;
+      int q = kFine - 1;
+      if constexpr (kSmallSh > 0) {
+        for (; q > 0; --q) {
+          if (acc + hf[g][q] >= rk[g]) break;
+          acc += hf[g][q];
+        }
+      }
+      uint32_t* sel = a.sel + (sw0 + g) * 4;
+      const uint32_t T = (uint32_t)(window_base<kSmallSh>(sel[2]) + (csl[g] << kSmallSh) + q);
+      sel[0] = T >> 8;
+      sel[2] = T;
+      sel[3] = jpw - (ab1[g] + acc);
+    }
+  }
+  __syncthreads();
+  const uint32_t miss = missm;
+  if (!miss) return;  // block-uniform
+  if (jpw < 4) {
+    // the last layer's groups (jpw = 2 at PROD): T is the (jpw+1)-th largest key, found by merging each
+    // lane's sorted top 4 across the wave and then the block (no histogram: a worker's values crowd into
+    // a few high-byte bins, where LDS atomics serialise)
+    __shared__ uint4 top[kKG][4];
+    {
+      ChunkScores cr;  // the chunk again (L2), all loads in flight at once
+      int wl = w0;
+      asm volatile("" : "+s"(wl));  // new addresses: CSE with the first pass's would keep them live throughout
+      load_chunk<false>(a, ci, wl, cr);
+      const LaneJobs lj = lane_jobs<false>(ci, cr);
+#pragma unroll
+      for (int g = 0; g < kKG; ++g) {
+        uint32_t k[4];
+#pragma unroll
+        for (int t = 0; t < kJPT; ++t) {
+          // + 0: okey needs one zero; a lane past the end (cost NaN) takes key 0, below every real key
+          const _Float16 x = lane_value(w0 + g, cr.v[t][g], lj.hb[t], lj.c[t]) + (_Float16)0.0f;
+          k[t] = lj.dead[t] ? 0u : okey(__builtin_bit_cast(uint16_t, x));
+        }
+        top4_sort(k);
+        lbuf[g * 256 + threadIdx.x] = make_uint2(k[0] | (k[1] << 16), k[2] | (k[3] << 16));
+      }
+    }
+    for (uint32_t m = miss; m; m &= m - 1u) {
+      const int g = __builtin_ctz(m);
+      const uint2 p = lbuf[g * 256 + threadIdx.x];
+      uint32_t k[4] = {p.x & 0xFFFFu, p.x >> 16, p.y & 0xFFFFu, p.y >> 16};
+      for (int o = 1; o < 64; o <<= 1) {
+        uint32_t q[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = (uint32_t)__shfl_xor((int)k[i], o);
+        top4_merge(k, q);
+      }
+      if (lane == 0) top[g][wv] = make_uint4(k[0], k[1], k[2], k[3]);
+    }
+    __syncthreads();
+    const int g = threadIdx.x;
+    if (g < kKG && ((miss >> g) & 1u)) {
+      uint32_t k[4] = {top[g][0].x, top[g][0].y, top[g][0].z, top[g][0].w};
+      for (int q = 1; q < 4; ++q) {
+        uint32_t o[4] = {top[g][q].x, top[g][q].y, top[g][q].z, top[g][q].w};
+        top4_merge(k, o);
+      }
+      const uint32_t T = k[jpw];
+      uint32_t gt = 0;
+      for (uint32_t i = 0; i < jpw; ++i) gt += k[i] > T;
+      uint32_t* sel = a.sel + (sw0 + g) * 4;
+      sel[0] = T >> 8;
+      sel[2] = T;
+      sel[3] = jpw - gt;
+    }
+    return;
+  }
   for (int pass = 0; pass < 2; ++pass) {
-    for (int i = threadIdx.x; i < kKG * 256; i += 256) (&h[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < kKG * kGStride; i += 256) h[i] = 0;
     __syncthreads();
     for (int t = 0; t < kJPT; ++t) {
       const int64_t jj = t * 256 + threadIdx.x;
@@ -614,20 +800,21 @@ __global__ __launch_bounds__(256) void sa_small_select_kernel(SegAuction a) {
       const uint16_t cj = a.cost[j];
       uint16_t v[kKG];
 #pragma unroll
-      for (int g = 0; g < kKG; ++g) v[g] = g < nw ? wrow(a, ci, w0 + g)[j] : 0;
+      for (int g = 0; g < kKG; ++g) v[g] = ((miss >> g) & 1u) ? wrow(a, ci, w0 + g)[j] : 0;
 #pragma unroll
       for (int g = 0; g < kKG; ++g) {
-        if (g >= nw) continue;
+        if (!((miss >> g) & 1u)) continue;
         const uint32_t k = okey(value_bits(w0 + g, v[g], hbj, cj));
-        if (pass == 0) atomicAdd(&h[g][k >> 8], 1u);
-        else if ((k >> 8) == b1s[g]) atomicAdd(&h[g][k & 255], 1u);
+        if (pass == 0) atomicAdd(&h[g * kGStride + (k >> 8)], 1u);
+        else if ((k >> 8) == b1s[g]) atomicAdd(&h[g * kGStride + (k & 255)], 1u);
       }
     }
     __syncthreads();
     for (int g = wv; g < nw; g += 4) {
+      if (!((miss >> g) & 1u)) continue;
       uint32_t b, above;
       const uint32_t rank = pass == 0 ? jpw + 1 : rk[g];
-      wave_select(h[g], rank, b, above);
+      wave_select(h + g * kGStride, rank, b, above);
       if (lane == 0) {
         if (pass == 0) {
           b1s[g] = b;
@@ -843,7 +1030,9 @@ __global__ __launch_bounds__(256) RQ_BID_ATTR void sa_bid_kernel(SegAuction a) {
   else bid_values<false>(cs, lj, nob, vT, vC, w0, epsh, best);
   if (straddle) {  // block-uniform: phase B's barrier is reached by every wave
     ChunkScores cr;  // the chunk again (L2-resident), so phase A keeps no values alive for this rare path
-    load_chunk<VEC>(a, ci, w0, cr);
+    int wl = w0;
+    asm volatile("" : "+s"(wl));  // new addresses: CSE with phase A's would keep them live throughout
+    load_chunk<VEC>(a, ci, wl, cr);
     uint32_t eqs[2] = {};
     equal_values(cr, lj, vT, straddle, w0, eqs);
     // straddling workers with an equal value in this wave (OR over the lanes); loops over worker bits
@@ -1089,6 +1278,9 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
                       hipMemsetAsync(a.above, 0, mk * kAbovePad * 4, st) != hipSuccess ||
                       hipMemsetAsync(a.miss, 1, mk, st) != hipSuccess ||
                       hipMemsetAsync(a.any_miss, 0, 4, st) != hipSuccess))
+    return fail(RQSID_E_LAUNCH, "seg_auction: memset");
+  // thresholds start at key 0 (a window of NaN keys: every worker takes the exact passes in round 0)
+  if (hipMemsetAsync(a.sel, 0, (size_t)n_seg * n_workers * 16, st) != hipSuccess)
     return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   hipLaunchKernelGGL(sa_job_init_kernel, dim3(grid_cap(cdiv(n_jobs, 256), 8192)), dim3(256), 0, st, a, n_jobs);
   const dim3 gcw((unsigned)total_chunks, (unsigned)cdiv(n_workers, kKG));

@@ -81,6 +81,24 @@ def test_seg_auction_against_oracle_and_active_mask():
         assert np.array_equal(a[lay.off[s]:lay.off[s + 1]], np.asarray(want, dtype=np.int64)), s
 
 
+@pytest.mark.parametrize("levels", [6, 3000])
+def test_seg_auction_small_groups_against_oracle(levels):
+    """The last layer's group shape (one-chunk segments with 2 or 3 jobs per worker: the block's top-4
+    merge selection whenever the guessed window misses), heavily tied and nearly tie-free; K=128 keeps
+    the oracle's 1002 rounds to seconds (the PROD groups have K=256, jpw=2)."""
+    k = 128
+    rng = np.random.default_rng(levels)
+    sizes = np.array([300, 3 * k + 1, 2 * k + 1], dtype=np.int64)
+    blocks = [_random_scores(rng, k, int(n), levels) for n in sizes]
+    flat = torch.from_numpy(np.concatenate([b.reshape(-1) for b in blocks])).to(DEV)
+    lay = ops.SegmentLayout(sizes, DEV)
+    a, rounds = ops.seg_auction(flat, k, lay)
+    a = a.cpu().numpy()
+    for s in range(len(sizes)):
+        want = O.auction_lap_half(blocks[s].T.astype(np.float32), tie_rule="stable")
+        assert np.array_equal(a[lay.off[s]:lay.off[s + 1]], np.asarray(want, dtype=np.int64)), s
+
+
 def _segments(sizes, seed):
     x = synth.small_mixture(int(np.sum(sizes)), m=24, seed=seed)
     return torch.from_numpy(x).to(DEV), ops.SegmentLayout(np.asarray(sizes, dtype=np.int64), DEV)
