@@ -33,6 +33,7 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
 from generative_ranking_recommender_amd import ops, synth  # noqa: E402
+from generative_ranking_recommender_amd.distributed import Comm  # noqa: E402
 from generative_ranking_recommender_amd.encode import HIERARCHICAL_TRAIN  # noqa: E402
 from generative_ranking_recommender_amd.hierarchical_rq_kmeans import (  # noqa: E402
     HierarchicalRQKMeans, HierarchicalRQKMeansConfig)
@@ -294,7 +295,7 @@ def train_iterations(x, c0, iters, world, n_global):
         tdist.barrier()
     el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=x.device)
     if world > 1:
-        tdist.all_reduce(el, op=tdist.ReduceOp.MAX)
+        Comm().all_reduce(el, op=tdist.ReduceOp.MAX)
     dt = float(el.item())
     return dt / iters * 1e3, n_global * iters / dt
 
@@ -322,7 +323,7 @@ def balanced_iterations(x, cb, rows, world=1):
             a, r = ShardedAuction().run(GpuAuctionPasses(w, rows * world), rows * world, k)
             sums, counts = ops.centroid_sums(xs, a.long(), k)
             buf = torch.cat([sums.reshape(-1), counts.to(sums.dtype)])
-            tdist.all_reduce(buf)
+            Comm().all_reduce(buf)
             return r
     else:
         def level0():
@@ -356,7 +357,7 @@ def balanced_iterations(x, cb, rows, world=1):
         if world > 1:
             import torch.distributed as tdist
             el = torch.tensor([dt], dtype=torch.float64, device=x.device)
-            tdist.all_reduce(el, op=tdist.ReduceOp.MAX)
+            Comm().all_reduce(el, op=tdist.ReduceOp.MAX)
             dt = float(el.item())
         tot = rows * (world if name == "level0" else 1)
         out[name] = {"ms_per_iteration": round(dt * 1e3, 2), "auction_rounds": int(r), "rows": tot,
@@ -387,10 +388,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
     import torch.distributed as tdist
+    # RQSID_BENCH_BACKEND=gloo: a rehearsal of the N-rank path on fewer GPUs (ranks share devices round-robin,
+    # host-staged collectives); the driver's multi-GPU runs use RCCL, one rank per GPU
+    backend = os.environ.get("RQSID_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     if dist:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
+        tdist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -455,7 +461,7 @@ def main():
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if dist:
-        tdist.all_reduce(el, op=tdist.ReduceOp.MAX)
+        Comm().all_reduce(el, op=tdist.ReduceOp.MAX)
     elapsed = float(el.item())
     ms = timer.mean_ms()
 
