@@ -6,4 +6,4 @@ import pytest
 def test_graft_entry_smoke(capsys):
     import __graft_entry__
     __graft_entry__.smoke()
-    assert "bit-identical to the oracle" in capsys.readouterr().out
+    assert "bit-identical to the exact oracle" in capsys.readouterr().out
