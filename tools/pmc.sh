@@ -17,3 +17,5 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
   echo "pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 "$OUT/p$i.log"; exit $rc; fi
 done
+python3 "$GRAFT_REPO_ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/summary.csv" && cat "$OUT/summary.csv"
+rm -rf "$OUT"/p*/  # the raw per-dispatch csvs exceed gpurun's merge-back cap
