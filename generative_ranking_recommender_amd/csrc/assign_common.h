@@ -107,16 +107,30 @@ __device__ __forceinline__ uint32_t lds_addr(const void* ptr) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)ptr;
 }
 
+// M0 around the LDS-DMA asm: saved and restored (RQ_M0_KEEP = 1, the default), or left clobbered
+// (0: two scalar instructions fewer per DMA; valid only while hipcc itself keeps nothing in M0 in these
+// kernels, which their ISA shows today)
+#ifndef RQ_M0_KEEP
+#define RQ_M0_KEEP 1
+#endif
+#if RQ_M0_KEEP
+#define RQ_M0_SAVE "s_mov_b32 %0, m0\n\t"
+#define RQ_M0_RESTORE "\n\ts_mov_b32 m0, %0"
+#else
+#define RQ_M0_SAVE ""
+#define RQ_M0_RESTORE ""
+#endif
+
 // One global_load_lds_dwordx4: every lane moves 16 B from its own global address to
 // lds_base + lane*16.  Inline asm keeps hipcc's waitcnt pass from draining the ring.
 __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_base) {
   uint32_t keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\t"
+      RQ_M0_SAVE
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
+      "global_load_lds_dwordx4 %1, off"
+      RQ_M0_RESTORE
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_base)
       : "memory");
@@ -127,11 +141,11 @@ template <int OFF>
 __device__ __forceinline__ void dma16_off(const void* gsrc, uint32_t lds_base) {
   uint32_t keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\t"
+      RQ_M0_SAVE
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off offset:%3\n\t"
-      "s_mov_b32 m0, %0"
+      "global_load_lds_dwordx4 %1, off offset:%3"
+      RQ_M0_RESTORE
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_base), "i"(OFF)
       : "memory");
@@ -140,11 +154,11 @@ template <int OFF>
 __device__ __forceinline__ void dma16_nt_off(const void* gsrc, uint32_t lds_base) {
   uint32_t keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\t"
+      RQ_M0_SAVE
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off offset:%3 nt\n\t"
-      "s_mov_b32 m0, %0"
+      "global_load_lds_dwordx4 %1, off offset:%3 nt"
+      RQ_M0_RESTORE
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_base), "i"(OFF)
       : "memory");
@@ -155,11 +169,11 @@ __device__ __forceinline__ void dma16_nt_off(const void* gsrc, uint32_t lds_base
 __device__ __forceinline__ void dma16_nt(const void* gsrc, uint32_t lds_base) {
   uint32_t keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\t"
+      RQ_M0_SAVE
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off nt\n\t"
-      "s_mov_b32 m0, %0"
+      "global_load_lds_dwordx4 %1, off nt"
+      RQ_M0_RESTORE
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_base)
       : "memory");
@@ -171,22 +185,22 @@ __device__ __forceinline__ void dma16_nt(const void* gsrc, uint32_t lds_base) {
 __device__ __forceinline__ void dma16_r(const void* gsrc, uint32_t lds_base) {
   uint32_t keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\t"
+      RQ_M0_SAVE
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
+      "global_load_lds_dwordx4 %1, off"
+      RQ_M0_RESTORE
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_base));
 }
 __device__ __forceinline__ void dma16_nt_r(const void* gsrc, uint32_t lds_base) {
   uint32_t keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\t"
+      RQ_M0_SAVE
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off nt\n\t"
-      "s_mov_b32 m0, %0"
+      "global_load_lds_dwordx4 %1, off nt"
+      RQ_M0_RESTORE
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_base));
 }

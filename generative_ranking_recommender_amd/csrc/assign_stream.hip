@@ -63,11 +63,11 @@ struct StreamLayout {
 __device__ __forceinline__ void dma4(const void* gsrc, uint32_t lds_base) {
   uint32_t keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\t"
+      RQ_M0_SAVE
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dword %1, off\n\t"
-      "s_mov_b32 m0, %0"
+      "global_load_lds_dword %1, off"
+      RQ_M0_RESTORE
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_base)
       : "memory");
