@@ -60,7 +60,7 @@ struct SegAuction {
   uint32_t* have;                // [S] jobs with a bidder this round
   int32_t* rounds;               // [S] rounds run (device)
   int32_t* round_dev;            // [1] the current round (device, so a captured block of rounds replays)
-  uint32_t* live_count;          // [1]
+  uint32_t* live_count;          // [3]: live segments, multi-chunk segments, a miss in a lean block
   uint16_t* cost;                // [N]
   int32_t* hb;                   // [N]
   uint8_t* nobid;                // [N]
@@ -86,6 +86,15 @@ struct SegAuction {
   uint16_t* chist;               // [K][total_chunks][256] each chunk's low-byte histogram of bin b1 from the
                                  // guessed pass: a hit worker's per-chunk tie count is entry T & 255
   uint32_t* any_miss;            // [1] some worker missed this round (the two-pass kernels exit at once if not)
+  // the round state at the start of a lean block (rounds without the two-pass kernels, replayed in full
+  // when a worker missed): costs, winners, no-bid flags, assignment, selections, segment flags and rounds
+  uint16_t* s_cost;
+  int32_t* s_hb;
+  uint8_t* s_nobid;
+  int32_t* s_out;
+  uint32_t* s_sel;
+  uint8_t* s_flag;
+  int32_t* s_rounds;
 };
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ off, int n_seg, int64_t i) {
@@ -604,7 +613,10 @@ __global__ __launch_bounds__(256) void sa_select_guess_kernel(SegAuction a) {
       sel[3] = jpw - (ab + above);
     }
     a.miss[hw] = hit ? 0 : 1;
-    if (!hit) *a.any_miss = 1;
+    if (!hit) {
+      *a.any_miss = 1;
+      a.live_count[2] = 1;  // a lean block that met a miss is replayed with the exact passes
+    }
     a.above[hw * kAbovePad] = 0;
   }
   for (int i = lane; i < 256; i += 64) h[i] = 0;
@@ -1124,6 +1136,43 @@ __global__ __launch_bounds__(256) void sa_round_end_kernel(SegAuction a, int cou
   if (count && (threadIdx.x & 63) == 0 && live) atomicAdd(a.live_count, live);
 }
 
+// copy the round state into (restore = 0) or back from (1) the lean block's snapshot
+__global__ __launch_bounds__(256) void sa_snapshot_kernel(SegAuction a, int32_t* __restrict__ out, int64_t n,
+                                                          int restore) {
+  const int64_t g0 = (int64_t)blockIdx.x * 256 + threadIdx.x, gs = (int64_t)gridDim.x * 256;
+  for (int64_t i = g0; i < n; i += gs) {
+    if (!restore) {
+      a.s_cost[i] = a.cost[i];
+      a.s_hb[i] = a.hb[i];
+      a.s_nobid[i] = a.nobid[i];
+      a.s_out[i] = out[i];
+    } else {
+      a.cost[i] = a.s_cost[i];
+      a.hb[i] = a.s_hb[i];
+      a.nobid[i] = a.s_nobid[i];
+      out[i] = a.s_out[i];
+    }
+  }
+  const int64_t ns = (int64_t)a.S * a.K * 4;
+  for (int64_t i = g0; i < ns; i += gs) {
+    if (!restore) a.s_sel[i] = a.sel[i];
+    else a.sel[i] = a.s_sel[i];
+  }
+  for (int64_t i = g0; i < a.S; i += gs) {
+    if (!restore) {
+      a.s_flag[i] = a.flag[i];
+      a.s_rounds[i] = a.rounds[i];
+    } else {
+      a.flag[i] = a.s_flag[i];
+      a.rounds[i] = a.s_rounds[i];
+    }
+  }
+  if (g0 == 0) {
+    if (!restore) a.s_sel[ns] = (uint32_t)*a.round_dev;
+    else *a.round_dev = (int32_t)a.s_sel[ns];
+  }
+}
+
 // multi-chunk segment ranks (one block): hidx[s] = rank or -1, mseg[rank] = s; live_count[1] = total
 __global__ __launch_bounds__(1024) void sa_multi_index_kernel(SegAuction a) {
   __shared__ uint32_t ws[16];
@@ -1173,7 +1222,7 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.eps = c.take<uint16_t>(S);
   a.mm = c.take<uint32_t>(2 * (int64_t)S);
   a.have = c.take<uint32_t>(S);
-  a.live_count = c.take<uint32_t>(2);
+  a.live_count = c.take<uint32_t>(4);
   a.round_dev = c.take<int32_t>(1);
   a.hidx = c.take<int32_t>(S);
   a.mseg = c.take<int32_t>(a.n_multi > 0 ? a.n_multi : 1);
@@ -1189,6 +1238,14 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.miss = guess ? c.take<uint8_t>((int64_t)a.n_multi * K) : nullptr;
   a.chist = guess && a.n_multi > 0 ? c.take<uint16_t>(total_chunks * K * 256) : nullptr;
   a.any_miss = guess ? c.take<uint32_t>(1) : nullptr;
+  const bool snap = guess && a.n_multi > 0;
+  a.s_cost = snap ? c.take<uint16_t>(N) : nullptr;
+  a.s_hb = snap ? c.take<int32_t>(N) : nullptr;
+  a.s_nobid = snap ? c.take<uint8_t>(N) : nullptr;
+  a.s_out = snap ? c.take<int32_t>(N) : nullptr;
+  a.s_sel = snap ? c.take<uint32_t>((int64_t)S * K * 4 + 1) : nullptr;  // + the round number
+  a.s_flag = snap ? c.take<uint8_t>(S) : nullptr;
+  a.s_rounds = snap ? c.take<int32_t>(S) : nullptr;
 }
 
 }  // namespace
@@ -1252,12 +1309,12 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   // pinned readback ([0] live segments, [1] multi-chunk segments): one buffer per host thread, kept
   // for the thread's lifetime (the lockstep fits call this once per iteration)
   static thread_local uint32_t* host = nullptr;
-  if (!host && hipHostMalloc((void**)&host, 2 * sizeof(uint32_t)) != hipSuccess) {
+  if (!host && hipHostMalloc((void**)&host, 4 * sizeof(uint32_t)) != hipSuccess) {
     host = nullptr;
     return fail(RQSID_E_LAUNCH, "seg_auction: pinned readback buffer");
   }
   int rc = RQSID_OK;
-  if (hipMemsetAsync(a.live_count, 0, 8, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "seg_auction: memset");
+  if (hipMemsetAsync(a.live_count, 0, 16, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   hipLaunchKernelGGL(sa_seg_init_kernel, dim3(gs), dim3(256), 0, st, a, active);
   hipLaunchKernelGGL(sa_multi_index_kernel, dim3(1), dim3(1024), 0, st, a);
   if ((rc = check_launch("seg_auction_init")) ||
@@ -1295,22 +1352,27 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   // into a counter zeroed after each read.  The round number lives on the device, so one captured block
   // (a HIP graph of kPoll rounds) replays for every block: the auction is launch-bound at small N.
   constexpr int kPoll = 8;
-  auto launch_round = [&](hipStream_t q, bool count) {
+  // lean rounds leave out the two-pass kernels of missed workers (five launches of a few us each, empty
+  // in most rounds); a lean block runs from a snapshot of the round state and is replayed with the full
+  // rounds when any worker missed in it, so the result is the full rounds' in every case
+  auto launch_round = [&](hipStream_t q, bool count, bool lean) {
     if (n_multi > 0) {
       if (vec) hipLaunchKernelGGL((sa_guess_hist_kernel<true>), gcw, dim3(256), 0, q, a);
       else hipLaunchKernelGGL((sa_guess_hist_kernel<false>), gcw, dim3(256), 0, q, a);
       hipLaunchKernelGGL(sa_select_guess_kernel, dim3(gmw), dim3(256), 0, q, a);
-      // the two-pass selection for the workers the guessed pass missed (every block exits at once
-      // when none of its workers missed)
-      if (vec) hipLaunchKernelGGL((sa_hist_kernel<0, true>), gcw, dim3(256), 0, q, a);
-      else hipLaunchKernelGGL((sa_hist_kernel<0, false>), gcw, dim3(256), 0, q, a);
-      hipLaunchKernelGGL((sa_select_kernel<false>), dim3(gmw), dim3(256), 0, q, a);
-      if (vec) hipLaunchKernelGGL((sa_hist_kernel<1, true>), gcw, dim3(256), 0, q, a);
-      else hipLaunchKernelGGL((sa_hist_kernel<1, false>), gcw, dim3(256), 0, q, a);
-      hipLaunchKernelGGL((sa_select_kernel<true>), dim3(gmw), dim3(256), 0, q, a);
-      if (vec) hipLaunchKernelGGL((sa_eqcount_kernel<true>), gcw, dim3(256), 0, q, a);
-      else hipLaunchKernelGGL((sa_eqcount_kernel<false>), gcw, dim3(256), 0, q, a);
-      hipLaunchKernelGGL(sa_eqscan_kernel, dim3(gmw), dim3(256), 0, q, a);
+      if (!lean) {
+        // the two-pass selection for the workers the guessed pass missed (every block exits at once
+        // when none of its workers missed)
+        if (vec) hipLaunchKernelGGL((sa_hist_kernel<0, true>), gcw, dim3(256), 0, q, a);
+        else hipLaunchKernelGGL((sa_hist_kernel<0, false>), gcw, dim3(256), 0, q, a);
+        hipLaunchKernelGGL((sa_select_kernel<false>), dim3(gmw), dim3(256), 0, q, a);
+        if (vec) hipLaunchKernelGGL((sa_hist_kernel<1, true>), gcw, dim3(256), 0, q, a);
+        else hipLaunchKernelGGL((sa_hist_kernel<1, false>), gcw, dim3(256), 0, q, a);
+        hipLaunchKernelGGL((sa_select_kernel<true>), dim3(gmw), dim3(256), 0, q, a);
+        if (vec) hipLaunchKernelGGL((sa_eqcount_kernel<true>), gcw, dim3(256), 0, q, a);
+        else hipLaunchKernelGGL((sa_eqcount_kernel<false>), gcw, dim3(256), 0, q, a);
+        hipLaunchKernelGGL(sa_eqscan_kernel, dim3(gmw), dim3(256), 0, q, a);
+      }
     }
     if (any_single) hipLaunchKernelGGL(sa_small_select_kernel, gcw, dim3(256), 0, q, a);
     if (vec) hipLaunchKernelGGL((sa_bid_kernel<true>), gcw, dim3(256), 0, q, a);
@@ -1318,45 +1380,75 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, q, a, out_assign);
     hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
   };
-  // capture one block on a private stream (the caller's may be the null stream, which cannot capture)
-  hipGraphExec_t exec = nullptr;
-  {
+  // capture blocks on a private stream (the caller's may be the null stream, which cannot capture)
+  auto capture = [&](bool lean) {
+    hipGraphExec_t ex = nullptr;
     hipStream_t cs = nullptr;
     hipGraph_t graph = nullptr;
     if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) == hipSuccess) {
       if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) == hipSuccess) {
-        for (int i = 0; i < kPoll; ++i) launch_round(cs, i == kPoll - 1);
+        for (int i = 0; i < kPoll; ++i) launch_round(cs, i == kPoll - 1, lean);
         if (hipStreamEndCapture(cs, &graph) == hipSuccess && graph) {
-          if (hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) != hipSuccess) exec = nullptr;
+          if (hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0) != hipSuccess) ex = nullptr;
           (void)hipGraphDestroy(graph);
         }
       }
       (void)hipStreamDestroy(cs);
     }
     (void)hipGetLastError();  // a failed capture falls back to direct launches
-  }
+    return ex;
+  };
+  hipGraphExec_t exec = capture(false);
+  hipGraphExec_t exec_lean = n_multi > 0 && exec ? capture(true) : nullptr;
+  const unsigned gsnap = (unsigned)grid_cap(cdiv(std::max<int64_t>(n_jobs, (int64_t)n_seg * n_workers * 4), 256), 4096);
   if (hipMemsetAsync(a.live_count, 0, 4, st) != hipSuccess) rc = fail(RQSID_E_LAUNCH, "seg_auction: memset");
+  bool try_lean = false;  // round 0 misses everywhere (thresholds start at key 0)
   for (int done = 0; rc == RQSID_OK && (max_rounds <= 0 || done < max_rounds);) {
     const int n = max_rounds > 0 ? std::min(kPoll, max_rounds - done) : kPoll;
-    if (exec && n == kPoll) {
+    const bool lean = try_lean && exec_lean && n == kPoll;
+    if (lean) {
+      hipLaunchKernelGGL(sa_snapshot_kernel, dim3(gsnap), dim3(256), 0, st, a, out_assign, n_jobs, 0);
+      if (hipMemsetAsync(a.live_count + 2, 0, 4, st) != hipSuccess || hipGraphLaunch(exec_lean, st) != hipSuccess) {
+        rc = fail(RQSID_E_LAUNCH, "seg_auction: graph launch");
+        break;
+      }
+    } else if (exec && n == kPoll) {
       if (hipGraphLaunch(exec, st) != hipSuccess) {
         rc = fail(RQSID_E_LAUNCH, "seg_auction: graph launch");
         break;
       }
     } else {
-      for (int i = 0; i < n; ++i) launch_round(st, i == n - 1);
+      for (int i = 0; i < n; ++i) launch_round(st, i == n - 1, false);
     }
-    done += n;
     if ((rc = check_launch("seg_auction_round"))) break;
-    if (hipMemcpyAsync(host, a.live_count, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+    if (hipMemcpyAsync(host, a.live_count, 12, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipMemsetAsync(a.live_count, 0, 4, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
       rc = fail(RQSID_E_LAUNCH, "seg_auction: readback");
       break;
     }
+    if (lean && host[2]) {
+      // a worker missed inside the lean block: back to its start, replay it with the exact passes
+      hipLaunchKernelGGL(sa_snapshot_kernel, dim3(gsnap), dim3(256), 0, st, a, out_assign, n_jobs, 1);
+      if (hipGraphLaunch(exec, st) != hipSuccess) {
+        rc = fail(RQSID_E_LAUNCH, "seg_auction: graph launch");
+        break;
+      }
+      if ((rc = check_launch("seg_auction_replay"))) break;
+      if (hipMemcpyAsync(host, a.live_count, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipMemsetAsync(a.live_count, 0, 4, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+        rc = fail(RQSID_E_LAUNCH, "seg_auction: readback");
+        break;
+      }
+      try_lean = false;
+    } else {
+      try_lean = n_multi > 0;
+    }
+    done += n;
     if (host[0] == 0) break;
     if (max_rounds > 0 && done >= max_rounds)
       rc = fail(RQSID_E_LAUNCH, "seg_auction: %u segments still bidding after %d rounds", host[0], max_rounds);
   }
+  if (exec_lean) (void)hipGraphExecDestroy(exec_lean);
   if (exec) (void)hipGraphExecDestroy(exec);
   return rc;
 }
