@@ -101,16 +101,95 @@ __global__ void centers_scale_kernel(float* __restrict__ scale) {
 #define RQSID_INTERLEAVE 0
 #endif
 
-template <int NT, int S, bool T3>
+constexpr int kSplitDim = 512;  // widest row of the candidate-split form
+// CW candidate groups (CW > 1: the candidate-split form, 4 CW waves, see assign_screen_kernel)
+template <int NT, int S, bool T3, int CW = 1>
 struct ScreenLayout {
-  static constexpr int kCHalf = NT * 32 * 64;              // NT*32 candidates x 32 fp16 dims
+  static constexpr int kCHalf = CW * NT * 32 * 64;         // CW*NT*32 candidates x 32 fp16 dims
   static constexpr int kCStage = kCHalf * (T3 ? 2 : 1);     // hi (+ lo) centre images
   static constexpr int kStage = kXStage + kCStage;
   static constexpr int kMeta = S * kStage;       // float4 {|c|^2, |c|, e0, 0} per candidate of the pass
-  static constexpr int kRes = kMeta + NT * 32 * 16;        // residual rows ca, cb (fp32, dim each)
-  static constexpr int bytes(int rl, int dim) { return kRes + rl * dim * 4; }
-  static constexpr int kMaxBytes = kRes + 2 * kMaxDim * 4;
+  // CW > 1 (single pass only): meta is the SoA |c|^2, |c| plus the per-wave maxima, and rows are at
+  // most kSplitDim wide, so a 3-stage ring of 48-KiB stages fits the 160 KiB of LDS
+  static constexpr int kRes = kMeta + (CW > 1 ? 2 * CW * NT * 32 * 4 + 256 : NT * 32 * 16);  // residual rows ca, cb
+  // CW > 1: the candidate groups' row exchange (least upper bounds, pass counts, merged lists)
+  static constexpr int kXch = kRes + 2 * (CW > 1 ? kSplitDim : kMaxDim) * 4;
+  static constexpr int kXchBytes = CW > 1 ? 2 * CW * kTileRows * 4 + kTileRows * kMaxList * 2 : 0;
+  static constexpr int bytes(int rl, int dim) { return CW > 1 ? kXch + kXchBytes : kRes + rl * dim * 4; }
+  static constexpr int kMaxBytes = kXch + kXchBytes;
+  static_assert(kMaxBytes <= 160 * 1024, "LDS budget");
 };
+
+// Row decision of the candidate-split form (CW groups of NT*32 candidates, one wave of each group per
+// 32 rows): pass_decide over every group's pass bits, exchanged through LDS.  Group g's candidates are
+// local positions g*NT*32 .. (g+1)*NT*32 - 1, so the groups' ascending lists concatenate in order.
+// k_out >= 0 only in the wave that holds a definitive row's single candidate; w (cand, n) is complete in
+// group 0's waves.  Contains two block barriers: every wave of the block calls it.
+template <int NW, int CW>
+__device__ __forceinline__ bool pass_decide_cw(const uint32_t (&pbits)[NW], int h, int cg, int rowt, int cgbase,
+                                               int& k_out, WorkItem& w, unsigned char* xch) {
+  int* xn = reinterpret_cast<int*>(xch + CW * kTileRows * 4);                    // [CW][128] counts, -1 overflow
+  uint16_t* xl = reinterpret_cast<uint16_t*>(xch + 2 * CW * kTileRows * 4);      // [128][kMaxList]
+  int pc = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) pc += __popc(pbits[i]);
+  const int pc_o = __shfl_xor(pc, 32);
+  const int nw = pc + pc_o;
+  const bool ovf_w = pc > kListPerHalf || pc_o > kListPerHalf;
+  uint32_t wv[NW];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) wv[i] = pbits[i];
+  const int k0 = pass_take_first(wv, h);
+  const int kw = max(k0, __shfl_xor(k0, 32));  // the group's candidate when nw == 1
+  if (h == 0) xn[cg * kTileRows + rowt] = ovf_w ? -1 : nw;
+  __syncthreads();
+  int total = 0, before = 0;
+  bool ovf = false;
+#pragma unroll
+  for (int g = 0; g < CW; ++g) {
+    const int n = xn[g * kTileRows + rowt];
+    ovf = ovf || n < 0;
+    total += max(n, 0);
+    before += g < cg ? max(n, 0) : 0;
+  }
+  ovf = ovf || total > kMaxList || total == 0;
+  const bool definitive = !ovf && total == 1;
+  k_out = definitive && nw == 1 ? cgbase + kw : -1;
+  w.n = ovf ? -1 : total;
+  const bool need_list = !ovf && total > 1;
+  if (__builtin_amdgcn_ballot_w64(need_list && nw > 0)) {  // wave-uniform: some row lists candidates here
+    int kk[kListPerHalf];
+    kk[0] = k0;
+#pragma unroll
+    for (int j = 1; j < kListPerHalf; ++j) kk[j] = pass_take_first(wv, h);
+    int c8[kMaxList];
+#pragma unroll
+    for (int j = 0; j < kListPerHalf; ++j) {
+      const int o = __shfl_xor(kk[j], 32);
+      c8[j] = kk[j] >= 0 ? kk[j] : INT_MAX;
+      c8[kListPerHalf + j] = o >= 0 ? o : INT_MAX;
+    }
+#pragma unroll
+    for (int i = 0; i < kMaxList; ++i)
+#pragma unroll
+      for (int j = 0; j < kMaxList - 1 - i; ++j) {
+        const int a = c8[j], bq = c8[j + 1];
+        c8[j] = min(a, bq);
+        c8[j + 1] = max(a, bq);
+      }
+    if (h == 0 && need_list) {
+#pragma unroll
+      for (int j = 0; j < kMaxList; ++j)
+        if (j < nw) xl[rowt * kMaxList + before + j] = (uint16_t)(cgbase + c8[j]);
+    }
+  }
+  __syncthreads();
+  if (cg == 0 && __builtin_amdgcn_ballot_w64(need_list)) {
+#pragma unroll
+    for (int j = 0; j < kMaxList; ++j) w.cand[j] = j < total ? xl[rowt * kMaxList + j] : (uint16_t)0xFFFF;
+  }
+  return definitive;
+}
 
 // Screening error model (DESIGN.md "Screening bound").  With v the row's vector, vh = fp16(v),
 // ex = v - vh, ch = fp16(c), ec = c - ch:
@@ -141,10 +220,18 @@ struct ScreenLayout {
 __device__ unsigned long long g_stamps_tile[8];
 #endif
 
-template <int NT, int S, int RL, bool NORM, bool T3, bool ONE>
-__global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <= 3) ? 2 : 1))) void assign_screen_kernel(AssignParams p) {
-  using L = ScreenLayout<NT, S, T3>;
-  constexpr int P = 4 + (NT / 2) * (T3 ? 2 : 1);  // DMA ops per wave per chunk (x: 4, centres: NT/2 per table)
+// Candidate-split form (CW > 1, single-pass segments only): 4 CW waves per block; wave w screens the
+// tile's rows 32 (w % 4) .. +31 against candidate group w / 4 (NT*32 candidates), so a segment of up to
+// CW*NT*32 candidates (the XL preset's 512 at the last level, 256 3-term at the middle one) is screened
+// in ONE pass: the tile's rows stream from HBM once instead of once per 256 / 128-candidate pass.  The
+// waves of a row group share the row image (each issues 4/CW of its DMAs) and exchange their least
+// upper bounds and pass lists through LDS (pass_decide_cw).
+template <int NT, int S, int RL, bool NORM, bool T3, bool ONE, int CW = 1>
+__global__ __launch_bounds__(256 * CW, CW > 1 ? 2 : (T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT == 4 && S <= 3) ? 2 : 1)))) void assign_screen_kernel(AssignParams p) {
+  static_assert(CW == 1 || (ONE && (CW == 2 || CW == 4)), "candidate-split form: single-pass segments");
+  using L = ScreenLayout<NT, S, T3, CW>;
+  constexpr int kXOps = 4 / CW;  // x-row DMA ops per wave per chunk (a row group's 4 split over its CW waves)
+  constexpr int P = kXOps + (NT / 2) * (T3 ? 2 : 1);  // DMA ops per wave per chunk (centres: NT/2 per table)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // FP16 (and FP64) denormals flushed: a row value below the fp16 normal range converts to 0 (its
   // value lands in the measured |v - vh|), so no subnormal operand reaches the MFMA (to_f16)
@@ -153,6 +240,8 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
 #endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rg = CW > 1 ? (wave & 3) : wave;   // row group: rows 32 rg .. 32 rg + 31 of the tile
+  const int cg = CW > 1 ? (wave >> 2) : 0;     // candidate group: local candidates cg NT 32 ..
   const int h = lane >> 5, r = lane & 31;
   ST(const uint64_t st_begin = ST_NOW(); uint64_t st_wait = 0; uint64_t st_e0 = 0; uint64_t st_issue = 0; uint64_t st_ring = 0;)
   // XCD-aware tile order: blocks b and b+8 share an XCD (and its L2), so give each group of 8 a
@@ -179,7 +268,7 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
   const bool penalty = p.seg_flags && (p.seg_flags[s] & RQSID_SEG_PENALTY);
   const int dim = p.dim;
 
-  const int my_local = wave * kRowsPerWave + r;
+  const int my_local = rg * kRowsPerWave + r;
   const bool row_valid = my_local < nrows;
   const int pos = t0 + (row_valid ? my_local : 0);
   const int my_row = p.row_index ? p.row_index[pos] : pos;
@@ -189,16 +278,17 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
     w.row = my_row;
     w.seg = s;
     w.n = penalty ? -2 : -3;
-    push_work(p, h == 0 && row_valid, lane, w);
+    push_work(p, cg == 0 && h == 0 && row_valid, lane, w);
     return;
   }
 
   // DMA sources for this wave's x rows: instruction i covers rows 8i + lane/8, 16-B slot lane%8 of the
-  // LDS image holding global slot (lane%8) ^ swz(row)  (swz(row) = (row>>1)&7: conflict-free reads)
-  const float* xsrc[4];
+  // LDS image holding global slot (lane%8) ^ swz(row)  (swz(row) = (row>>1)&7: conflict-free reads);
+  // CW > 1: the row group's instructions cg*kXOps .. +kXOps-1
+  const float* xsrc[kXOps];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int rr = 8 * i + (lane >> 3);
+  for (int i = 0; i < kXOps; ++i) {
+    const int rr = 8 * (cg * kXOps + i) + (lane >> 3);
     const int grow = __shfl(my_row, rr);
     const int slot = (lane & 7) ^ ((rr >> 1) & 7);
     xsrc[i] = p.x + (int64_t)grow * dim + slot * 4;
@@ -210,11 +300,11 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
   auto stage_residual_rows = [&]() {
     if (RL >= 1) {
       const float4* a = reinterpret_cast<const float4*>(p.ca + (int64_t)seg_row(p.seg_ca, s) * dim);
-      for (int i = tid; i < dim / 4; i += 256) reinterpret_cast<float4*>(lds_ca)[i] = a[i];
+      for (int i = tid; i < dim / 4; i += 256 * CW) reinterpret_cast<float4*>(lds_ca)[i] = a[i];
     }
     if (RL >= 2) {
       const float4* a = reinterpret_cast<const float4*>(p.cb + (int64_t)seg_row(p.seg_cb, s) * dim);
-      for (int i = tid; i < dim / 4; i += 256) reinterpret_cast<float4*>(lds_cb)[i] = a[i];
+      for (int i = tid; i < dim / 4; i += 256 * CW) reinterpret_cast<float4*>(lds_cb)[i] = a[i];
     }
     if (RL >= 2 && NORM) inv1 = 1.0f / p.den_in[my_row];
     asm volatile("" : "+v"(inv1));  // its load completes before the ring's compute starts
@@ -241,8 +331,8 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
 
   const int npass = ONE ? 1 : (cnt + NT * 32 - 1) / (NT * 32);
   float* m_csq = reinterpret_cast<float*>(smem + L::kMeta);  // ONE: SoA meta |c|^2, |c|, per-wave maxima
-  float* m_y = m_csq + NT * 32;
-  float* m_red = m_y + NT * 32;
+  float* m_y = m_csq + CW * NT * 32;
+  float* m_red = m_y + CW * NT * 32;
   uint32_t pbits[ONE ? NT / 2 : 1];  // ONE: pass bits, word w = tiles 2w, 2w+1, MSB first
   for (int pass = 0; pass < npass; ++pass) {
     const int pbase = pass * NT * 32;
@@ -264,12 +354,12 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
     // DMA op i of chunk c (x rows 0..3, hi centres, lo centres) into stage c % S
     auto issue_op = [&](int c, int i, bool relaxed) {
       const uint32_t sb = lds0 + (uint32_t)((c % S) * L::kStage);
-      if (i < 4) {
+      if (i < kXOps) {
         const void* src = xsrc[i] + c * kChunk;
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(sb + wave * kXWaveBytes + i * 1024);
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(sb + rg * kXWaveBytes + (cg * kXOps + i) * 1024);
         if (relaxed) dma16_nt_r(src, dst); else dma16_nt(src, dst);
       } else {
-        const int j = i - 4;
+        const int j = i - kXOps;
         const void* src = csrc[j] + c * kCStride;
         const uint32_t dst = __builtin_amdgcn_readfirstlane(sb + kXStage + (wave * kCOps + j) * 1024);
         if (relaxed) dma16_r(src, dst); else dma16(src, dst);
@@ -291,7 +381,7 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
     }
     if constexpr (ONE) {
       float gz = 0.f, gw = 0.f, gy = 0.f;
-      if (tid < NT * 32) {
+      if (tid < CW * NT * 32) {
         const bool live = pbase + tid < cnt;
         const int kl = live ? pbase + tid : cnt - 1;
         const float4 m = reinterpret_cast<const float4*>(p.c_meta)[cand_global(p, cbase, kl)];
@@ -338,9 +428,9 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
       return;
 #endif
       constexpr int NG = 2 * NT;
-      const unsigned char* xb = smem + (c % S) * L::kStage + wave * kXWaveBytes + r * 128;
+      const unsigned char* xb = smem + (c % S) * L::kStage + rg * kXWaveBytes + r * 128;
       // centre image row of candidate t*32 + r: 64 B (1 term) or 128 B (T3: hi slots 0-3, lo 4-7)
-      const unsigned char* cbp = smem + (c % S) * L::kStage + kXStage + r * (T3 ? 128 : 64);
+      const unsigned char* cbp = smem + (c % S) * L::kStage + kXStage + (cg * NT * 32 + r) * (T3 ? 128 : 64);
       const int tsw = (r >> 1) & 7;  // T3 image swizzle (the x image's)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -421,7 +511,7 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
         }
         const float den = nrm + 1e-8f;
         inv_den = 1.0f / den;
-        if (RL == 1 && h == 0 && row_valid && p.den_out) p.den_out[my_row] = den;
+        if (RL == 1 && cg == 0 && h == 0 && row_valid && p.den_out) p.den_out[my_row] = den;
         // |r_ref - v/den| per element: RL1: the reference rounds r_i = u_i/den once;
         // RL2: v was built with a reciprocal multiply (2 ulp of |r1| = 1) and rounded
         // RL2 also: the fp32 denominator's error, |v/den' - v/den| <= den_eps |v| / den'
@@ -463,7 +553,7 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
     if constexpr (ONE) {
       float gz = 0.f, gw = 0.f, gy = 0.f;
 #pragma unroll
-      for (int w = 0; w < kWaves; ++w) {
+      for (int w = 0; w < kWaves * CW; ++w) {
         gz = fmaxf(gz, m_red[w * 4 + 0]);
         gw = fmaxf(gw, m_red[w * 4 + 1]);
         gy = fmaxf(gy, m_red[w * 4 + 2]);
@@ -476,8 +566,8 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const float4 cs = *reinterpret_cast<const float4*>(m_csq + t * 32 + 8 * g + 4 * h);
-          const float4 yy = *reinterpret_cast<const float4*>(m_y + t * 32 + 8 * g + 4 * h);
+          const float4 cs = *reinterpret_cast<const float4*>(m_csq + (cg * NT + t) * 32 + 8 * g + 4 * h);
+          const float4 yy = *reinterpret_cast<const float4*>(m_y + (cg * NT + t) * 32 + 8 * g + 4 * h);
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             const int v = 4 * g + 2 * e;
@@ -493,6 +583,17 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
         }
       }
       U = fminf(U, __shfl_xor(U, 32));
+      if constexpr (CW > 1) {  // the row's least upper bound over every candidate group
+        // lb materialised here: otherwise hipcc sinks lb = P - E past the barrier, keeping P and E
+        // both live (256 VGPRs -> spills)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) asm volatile("" : "+v"(acc[t]));
+        float* xu = reinterpret_cast<float*>(smem + L::kXch);
+        if (h == 0) xu[cg * kTileRows + my_local] = U;
+        __syncthreads();
+#pragma unroll
+        for (int g = 0; g < CW; ++g) U = fminf(U, xu[g * kTileRows + my_local]);
+      }
       // sweep 2: one bit per candidate, lb <= U, i.e. the sign of lb - Up with Up > U by >= 2 ulp (a
       // candidate admitted by rounding is only re-scored); v_alignbit shifts the sign into the word.
       // v = 0..15 is ascending in candidate order, so word w holds tile 2w's candidates from bit 31
@@ -570,12 +671,14 @@ __global__ __launch_bounds__(256, T3 ? 2 : (S == 2 ? (NT == 4 ? 3 : 2) : ((NT ==
     w.row = my_row;
     w.seg = s;
     int k = -1;
-    const bool definitive = pass_decide(pbits, h, k, w);
-    if (h == 0 && row_valid && definitive) {
+    bool definitive;
+    if constexpr (CW > 1) definitive = pass_decide_cw<NT / 2, CW>(pbits, h, cg, my_local, cg * NT * 32, k, w, smem + L::kXch);
+    else definitive = pass_decide(pbits, h, k, w);
+    if (h == 0 && row_valid && definitive && k >= 0) {
       p.out_local[my_row] = cand_local(p, cbase, k);
       p.out_global[my_row] = cand_global(p, cbase, k);
     }
-    push_work(p, h == 0 && row_valid && !definitive, lane, w);
+    push_work(p, cg == 0 && h == 0 && row_valid && !definitive, lane, w);
 #ifdef RQSID_STAMPS
     if (tid == 0) {
       const uint64_t now = ST_NOW();
@@ -880,14 +983,14 @@ __global__ __launch_bounds__(64) void mfma_probe_kernel(const uint16_t* __restri
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-template <int NT, int S, bool T3, bool ONE>
+template <int NT, int S, bool T3, bool ONE, int CW = 1>
 void set_attrs(bool* ok) {
-  const int bytes = ScreenLayout<NT, S, T3>::kMaxBytes;
-  const void* ks[] = {(const void*)assign_screen_kernel<NT, S, 0, false, T3, ONE>,
-                      (const void*)assign_screen_kernel<NT, S, 1, false, T3, ONE>,
-                      (const void*)assign_screen_kernel<NT, S, 1, true, T3, ONE>,
-                      (const void*)assign_screen_kernel<NT, S, 2, false, T3, ONE>,
-                      (const void*)assign_screen_kernel<NT, S, 2, true, T3, ONE>};
+  const int bytes = ScreenLayout<NT, S, T3, CW>::kMaxBytes;
+  const void* ks[] = {(const void*)assign_screen_kernel<NT, S, 0, false, T3, ONE, CW>,
+                      (const void*)assign_screen_kernel<NT, S, 1, false, T3, ONE, CW>,
+                      (const void*)assign_screen_kernel<NT, S, 1, true, T3, ONE, CW>,
+                      (const void*)assign_screen_kernel<NT, S, 2, false, T3, ONE, CW>,
+                      (const void*)assign_screen_kernel<NT, S, 2, true, T3, ONE, CW>};
   for (const void* k : ks)
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) *ok = false;
 }
@@ -899,6 +1002,13 @@ int screen_variant() {  // read per call: tests switch it within one process
   const char* e = getenv("RQSID_SCREEN_VARIANT");
   return e ? atoi(e) : 0;
 }
+
+// ring depth of the candidate-split form: one block per CU, so its chunks in flight are the CU's
+// (latency-bound at S = 2: 48 KiB in flight per CU)
+#ifndef RQSID_SPLIT_S
+#define RQSID_SPLIT_S 3
+#endif
+constexpr int kSplitS = RQSID_SPLIT_S;
 
 bool g_attr_done[kMaxDevices] = {};
 int ensure_attrs() {
@@ -912,19 +1022,22 @@ int ensure_attrs() {
   set_attrs<4, 2, false, false>(&ok);
   set_attrs<8, 2, false, false>(&ok);
   set_attrs<4, 2, true, false>(&ok);
+  set_attrs<8, kSplitS, false, true, 2>(&ok);
+  set_attrs<4, kSplitS, true, true, 2>(&ok);
   if (!ok) return fail(RQSID_E_LAUNCH, "assign: cannot raise the dynamic LDS limit");
   g_attr_done[dev] = true;
   return RQSID_OK;
 }
 
-template <int NT, int S, bool T3, bool ONE>
+template <int NT, int S, bool T3, bool ONE, int CW = 1>
 void launch_screen(const AssignParams& p, int rl, bool norm, unsigned grid, hipStream_t st) {
-  const size_t lds = ScreenLayout<NT, S, T3>::bytes(rl, p.dim);
-  if (rl == 0) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 0, false, T3, ONE>), dim3(grid), dim3(256), lds, st, p);
-  else if (rl == 1 && norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, true, T3, ONE>), dim3(grid), dim3(256), lds, st, p);
-  else if (rl == 1) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, false, T3, ONE>), dim3(grid), dim3(256), lds, st, p);
-  else if (norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, true, T3, ONE>), dim3(grid), dim3(256), lds, st, p);
-  else hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, false, T3, ONE>), dim3(grid), dim3(256), lds, st, p);
+  const size_t lds = ScreenLayout<NT, S, T3, CW>::bytes(rl, p.dim);
+  const dim3 blk(256 * CW);
+  if (rl == 0) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 0, false, T3, ONE, CW>), dim3(grid), blk, lds, st, p);
+  else if (rl == 1 && norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, true, T3, ONE, CW>), dim3(grid), blk, lds, st, p);
+  else if (rl == 1) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 1, false, T3, ONE, CW>), dim3(grid), blk, lds, st, p);
+  else if (norm) hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, true, T3, ONE, CW>), dim3(grid), blk, lds, st, p);
+  else hipLaunchKernelGGL((assign_screen_kernel<NT, S, 2, false, T3, ONE, CW>), dim3(grid), blk, lds, st, p);
 }
 template <int NT, int S, bool T3>
 void launch_screen2(const AssignParams& p, int rl, bool norm, unsigned grid, bool one, hipStream_t st) {
@@ -1087,10 +1200,16 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
       p.tile_seg = tile_seg;
     }
   }
+  // candidate-split single pass (CW = 2) for segments wider than one wave's tiles: 3-term <= 256
+  // candidates, 1-term <= 512 (the XL preset's middle and last levels); RQSID_SCREEN_VARIANT=7 (or 2)
+  // keeps the multi-pass screen for comparison
+  const bool split = !legacy && variant != 7 && dim <= kSplitDim;
   if (use_stream || use_res) {
-  } else if (t3) launch_screen2<4, 2, true>(p, res_levels, norm, grid, !legacy && cand_count_max <= 128, st);
+  } else if (t3 && cand_count_max > 128 && split) launch_screen<4, kSplitS, true, true, 2>(p, res_levels, norm, grid, st);
+  else if (t3) launch_screen2<4, 2, true>(p, res_levels, norm, grid, !legacy && cand_count_max <= 128, st);
   else if (cand_count_max <= 128) launch_screen2<4, 2, false>(p, res_levels, norm, grid, !legacy, st);
   else if (cand_count_max <= 256) launch_screen2<8, 2, false>(p, res_levels, norm, grid, !legacy, st);
+  else if (cand_count_max <= 512 && split) launch_screen<8, kSplitS, false, true, 2>(p, res_levels, norm, grid, st);
   else launch_screen<8, 2, false, false>(p, res_levels, norm, grid, st);
   if ((rc = check_launch("assign_screen"))) return rc;
   const dim3 g(4096);  // multiple of 8 (XCD-grouped work runs)

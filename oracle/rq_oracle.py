@@ -122,7 +122,14 @@ def exact_d2(x: np.ndarray, c: np.ndarray) -> np.ndarray:
     """fp64 squared distances (the arbiter for near ties)."""
     x = x.astype(np.float64)
     c = c.astype(np.float64)
-    return (x * x).sum(1)[:, None] + (c * c).sum(1)[None, :] - 2.0 * (x @ c.T)
+    d = (x * x).sum(1)[:, None] + (c * c).sum(1)[None, :] - 2.0 * (x @ c.T)
+    # identical centres have identical exact distances; the blocked GEMM can round their columns
+    # differently, so duplicates copy their first occurrence's column (exact ties -> lowest index)
+    _, first, inv = np.unique(c, axis=0, return_index=True, return_inverse=True)
+    src = first[inv.reshape(-1)]
+    if (src != np.arange(len(c))).any():
+        d = d[:, src]
+    return d
 
 
 def _dist(x: np.ndarray, c: np.ndarray, exact: bool) -> np.ndarray:

@@ -475,3 +475,44 @@ def test_resident_spin_cap_fails_loudly():
                     lambda: ops.nearest(gpu(x), pc).cpu().numpy())
     sel = np.arange(0, 30000, 29)
     assert (got[sel] == exact_ids(x[sel], c)).all()
+
+
+MULTI_PASS = {"RQSID_SCREEN_VARIANT": 7}  # the multi-pass per-tile screen, no candidate split
+
+
+@pytest.mark.parametrize("k,terms", [(257, 1), (384, 1), (512, 1), (129, 3), (200, 3), (256, 3)])
+def test_candidate_split_nearest(k, terms):
+    """Candidate-split single-pass screen (CW = 2: 512 1-term / 256 3-term candidates per segment):
+    identical to the multi-pass screen and to the exact oracle, including partly padded candidate
+    groups and duplicated centres (exact ties: lowest index)."""
+    rng = np.random.default_rng(1000 + k + terms)
+    c = rng.standard_normal((k, 512)).astype(np.float32)
+    c[k - 1] = c[3]  # a duplicate in the second group: ties across the groups resolve to the lower index
+    x = (c[rng.integers(0, k, 20000)] + 0.3 * rng.standard_normal((20000, 512))).astype(np.float32)
+    x[:64] = c[3]    # rows sitting exactly on the duplicated centre
+    pc = ops.prepare_centers(gpu(c))
+    got = ops.nearest(gpu(x), pc, screen_terms=terms).cpu().numpy()
+    multi = _with_env(MULTI_PASS, lambda: ops.nearest(gpu(x), pc, screen_terms=terms).cpu().numpy())
+    assert (got == multi).all(), f"{int((got != multi).sum())} rows differ from the multi-pass screen"
+    assert (got[:64] == 3).all()
+    sel = np.arange(0, 20000, 13)
+    assert (got[sel] == exact_ids(x[sel], c)).all()
+
+
+def test_candidate_split_xl_levels_equal_multi_pass():
+    """XL shapes (need [256,256,512]): the middle level (256 3-term candidates per parent) and the last
+    level (512 per group) take the candidate-split screen; every level's IDs equal the multi-pass
+    screen's, and a sample equals the exact oracle."""
+    need = (256, 256, 512)
+    cb = synth.encode_codebooks(seed=5, need=need, n_cand=5120)
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], list(need),
+                    match=torch.from_numpy(cb["match"]), semantics=HIERARCHICAL_TRAIN, device=DEV)
+    xn = synth.mixture_rows(3, 120000)
+    x = gpu(xn)
+    a = enc.encode(x).cpu().numpy()
+    b = _with_env(MULTI_PASS, lambda: enc.encode(x).cpu().numpy())
+    assert (a == b).all(), f"{int((a != b).any(1).sum())} rows differ between the split and multi-pass screens"
+    sel = np.arange(0, 120000, 97)
+    ref = O.encode(xn[sel], [cb["c0"], cb["c1"], cb["c2"]], list(need), cb["match"], residual_from_weighted=True,
+                   exact=True)
+    assert (a[sel] == ref).all()
