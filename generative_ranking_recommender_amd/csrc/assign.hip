@@ -1003,10 +1003,10 @@ int screen_variant() {  // read per call: tests switch it within one process
   return e ? atoi(e) : 0;
 }
 
-// ring depth of the candidate-split form: one block per CU, so its chunks in flight are the CU's
-// (latency-bound at S = 2: 48 KiB in flight per CU)
+// ring depth of the candidate-split form (one block per CU).  S = 3 (96 KiB in flight per CU instead of
+// 48) measured no faster on the XL levels (L2 15.3 vs 14.8 ms), so the smaller ring stays
 #ifndef RQSID_SPLIT_S
-#define RQSID_SPLIT_S 3
+#define RQSID_SPLIT_S 2
 #endif
 constexpr int kSplitS = RQSID_SPLIT_S;
 
