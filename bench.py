@@ -23,6 +23,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -66,6 +67,9 @@ def parse():
                     help="rows of the balanced (auction) training iterations in 'train_balanced' (0 = skip)")
     ap.add_argument("--train-iters", type=int, default=3,
                     help="Lloyd iterations timed for the 'train' field (0 = skip)")
+    ap.add_argument("--side-budget", type=float, default=0.0,
+                    help="seconds the side measurements after the timed region may take before the encode line is "
+                         "printed without the rest and every rank exits (0: 600 at N=1, 300 at N>1)")
     ap.add_argument("--config0", type=int, default=1,
                     help="1: also run BASELINE configs[0] (100k, single level K=128, simplified path) on the GPU and "
                          "its CPU restatement on a bounded sample (field 'config0')")
@@ -536,6 +540,29 @@ def main():
     }
     if gather_ms is not None:
         line["gather_ids_ms"] = round(gather_ms, 3) if isinstance(gather_ms, float) else {"error": gather_ms}
+    # The encode line is complete here.  The side measurements below run collectives at N > 1; a hang
+    # there must not cost the line: a watchdog prints what is measured so far and ends every rank.
+    printed, plock = threading.Event(), threading.Lock()
+
+    def watchdog():
+        budget = args.side_budget or (600.0 if world == 1 else 300.0)
+        if printed.wait(budget):
+            return
+        with plock:  # exactly one line: the main thread prints under the same lock
+            if printed.is_set():
+                return
+            printed.set()
+            if rank == 0:
+                try:
+                    snap = dict(line)
+                    snap["side_measurements"] = f"stopped after {budget:.0f} s (watchdog)"
+                    print(json.dumps(snap), flush=True)
+                except Exception:
+                    pass
+            sys.stdout.flush()
+            os._exit(0)
+
+    threading.Thread(target=watchdog, daemon=True).start()
     if args.train_iters > 0:
         try:
             t_ms, rps = train_iterations(x, torch.from_numpy(cb["c0"]).to(dev).float(), args.train_iters, world,
@@ -560,8 +587,12 @@ def main():
             line["config0"] = config0(dev)
         except Exception as exc:  # a side measurement must not cost the encode line
             line["config0"] = {"error": repr(exc)[:300]}
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+    with plock:
+        if printed.is_set():
+            return
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        printed.set()
     if dist:
         tdist.destroy_process_group()
 
