@@ -896,6 +896,155 @@ __global__ __launch_bounds__(256) void assign_rescore_kernel(AssignParams p) {
   }
 }
 
+// Two listed rows per wave (rows of at most kHalfDim dims): lanes 32 hh .. 32 hh + 31 re-score item
+// 2 wid + hh of the pass with 4 float4 of the row per lane; the same arithmetic, candidate batches and
+// (distance, index) rule as assign_rescore_kernel, with every reduction kept inside the half.  The
+// re-score is bound by its dependent-load chain (item -> row, residual rows -> candidate rows), not by
+// bytes, and a wave now carries two chains at the same register count.
+constexpr int kHalfDim = 512;
+__device__ __forceinline__ double half_sum(double v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <int RL, bool NORM>
+__global__ __launch_bounds__(256) void assign_rescore_half_kernel(AssignParams p) {
+  constexpr int kV = kHalfDim / 128;  // float4 per lane
+  const int lane = threadIdx.x & 63, hl = lane & 31, hh = lane >> 5;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nw = gridDim.x * 4;
+  const int64_t nitems_raw = *p.work_count;
+  const int64_t nitems = nitems_raw < p.work_cap ? nitems_raw : p.work_cap;
+  const int nv = p.dim / 4;
+  for (int64_t it0 = 2 * (int64_t)wid; it0 < nitems; it0 += 2 * (int64_t)nw) {
+    const bool active = it0 + hh < nitems;  // an idle half repeats its partner's item and writes nothing
+    const int64_t it = active ? it0 + hh : it0;
+    const WorkItem w = p.work[p.work_idx ? p.work_idx[it] : it];
+    const float* xr = p.x + (int64_t)w.row * p.dim;
+    const float* car = RL >= 1 ? p.ca + (int64_t)seg_row(p.seg_ca, w.seg) * p.dim : nullptr;
+    const float* cbr = RL >= 2 ? p.cb + (int64_t)seg_row(p.seg_cb, w.seg) * p.dim : nullptr;
+    const bool screened = w.n >= 1 || w.n == -1;  // the screen wrote den_out for these rows
+    float4 v[kV];
+    double ss = 0.0;
+#pragma unroll
+    for (int m = 0; m < kV; ++m) {
+      const int i = hl + 32 * m;
+      if (i < nv) {
+        float4 a = reinterpret_cast<const float4*>(xr)[i];
+        if (RL >= 1) {
+          const float4 c = reinterpret_cast<const float4*>(car)[i];
+          a = make_float4(a.x - c.x, a.y - c.y, a.z - c.z, a.w - c.w);
+        }
+        if (RL >= 2) {
+          if (NORM) {
+            const float d1 = p.den_in[w.row];
+            a = make_float4(a.x / d1, a.y / d1, a.z / d1, a.w / d1);
+          }
+          const float4 c = reinterpret_cast<const float4*>(cbr)[i];
+          a = make_float4(a.x - c.x, a.y - c.y, a.z - c.z, a.w - c.w);
+        }
+        v[m] = a;
+        ss += (double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z + (double)a.w * a.w;
+      } else {
+        v[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    if (NORM && RL >= 1) {
+      float den;
+      if (RL == 1 && p.den_out && screened) den = p.den_out[w.row];
+      else den = (float)sqrt(half_sum(ss)) + 1e-8f;
+      if (RL == 1 && p.den_out && !screened && hl == 0 && active) p.den_out[w.row] = den;
+#pragma unroll
+      for (int m = 0; m < kV; ++m)
+        v[m] = make_float4(v[m].x / den, v[m].y / den, v[m].z / den, v[m].w / den);
+    }
+    const bool penalty = w.n == -2;
+    const bool listed = w.n >= 1;
+    const int base = p.cand_base[w.seg];
+    const int n = listed ? w.n : (penalty ? p.n_centers : (w.n == -1 ? p.cand_count[w.seg] : 0));
+    const int nmax = max(n, __shfl_xor(n, 32));  // both halves run the same batches
+    double best = INFINITY;
+    int bj = INT_MAX;
+    for (int j0 = 0; j0 < nmax; j0 += kBatch) {
+      double acc[kBatch];
+      int loc[kBatch];
+#pragma unroll
+      for (int jj = 0; jj < kBatch; ++jj) {
+        const int j = j0 + jj;
+        acc[jj] = 0.0;
+        loc[jj] = j < n ? (listed ? (int)w.cand[jj] : j) : INT_MAX;
+        if (j < n) {
+          const int g = penalty ? loc[jj] : cand_global(p, base, loc[jj]);
+          const float4* cr = reinterpret_cast<const float4*>(p.centers + (int64_t)g * p.dim);
+#pragma unroll
+          for (int m = 0; m < kV; ++m) {
+            const int i = hl + 32 * m;
+            if (i < nv) {
+              const float4 c = cr[i];
+              const double d0 = (double)v[m].x - c.x, d1 = (double)v[m].y - c.y, d2 = (double)v[m].z - c.z,
+                           d3 = (double)v[m].w - c.w;
+              acc[jj] += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+            }
+          }
+        }
+      }
+      // halving reduction inside the half: 4 + 2 + 1 exchanges leave lane hl holding candidate
+      // jj(hl) = 4*((hl>>4)&1) + 2*((hl>>3)&1) + ((hl>>2)&1) summed over its 4-lane group; 2 more finish it
+      double r4[4], r2[2], r1;
+      const bool b4 = hl & 16, b3 = hl & 8, b2 = hl & 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double send = b4 ? acc[j] : acc[j + 4];
+        const double keep = b4 ? acc[j + 4] : acc[j];
+        r4[j] = keep + __shfl_xor(send, 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const double send = b3 ? r4[j] : r4[j + 2];
+        const double keep = b3 ? r4[j + 2] : r4[j];
+        r2[j] = keep + __shfl_xor(send, 8);
+      }
+      {
+        const double send = b2 ? r2[0] : r2[1];
+        const double keep = b2 ? r2[1] : r2[0];
+        r1 = keep + __shfl_xor(send, 4);
+      }
+      r1 += __shfl_xor(r1, 2);
+      r1 += __shfl_xor(r1, 1);
+      const int my_jj = 4 * ((hl >> 4) & 1) + 2 * ((hl >> 3) & 1) + ((hl >> 2) & 1);
+      int my_loc = INT_MAX;
+#pragma unroll
+      for (int jj = 0; jj < kBatch; ++jj) my_loc = my_jj == jj ? loc[jj] : my_loc;
+      double key = r1;
+      if (penalty) key = (double)((float)sqrt((double)(float)key) + 10000.0f);
+#pragma unroll
+      for (int o = 4; o < 32; o <<= 1) {
+        const double ok = __shfl_xor(key, o);
+        const int ol = __shfl_xor(my_loc, o);
+        const bool kn = key != key, okn = ok != ok;
+        const bool take = ol != INT_MAX && (my_loc == INT_MAX || (!okn && (kn || ok < key || (ok == key && ol < my_loc))));
+        key = take ? ok : key;
+        my_loc = take ? ol : my_loc;
+      }
+      {
+        const bool kn = key != key, bn = best != best;
+        const bool take = my_loc != INT_MAX &&
+                          (bj == INT_MAX || (!kn && (bn || key < best || (key == best && my_loc < bj))));
+        if (take) {
+          best = key;
+          bj = my_loc;
+        }
+      }
+    }
+    if (hl == 0 && active) {
+      const bool found = bj != INT_MAX;
+      p.out_local[w.row] = found && !penalty ? cand_local(p, base, bj) : -1;
+      p.out_global[w.row] = found ? (penalty ? bj : cand_global(p, base, bj)) : -1;
+    }
+  }
+}
+
 // tile -> segment map of the per-tile screen (one thread per tile, binary search of seg_tile_off)
 __global__ __launch_bounds__(256) void tile_seg128_kernel(const int32_t* __restrict__ seg_tile_off, int nseg,
                                                           int64_t cap, int32_t* __restrict__ tile_seg) {
@@ -1213,11 +1362,20 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   else launch_screen<8, 2, false, false>(p, res_levels, norm, grid, st);
   if ((rc = check_launch("assign_screen"))) return rc;
   const dim3 g(4096);  // multiple of 8 (XCD-grouped work runs)
-  if (res_levels == 0) hipLaunchKernelGGL((assign_rescore_kernel<0, false>), g, dim3(256), 0, st, p);
-  else if (res_levels == 1 && norm) hipLaunchKernelGGL((assign_rescore_kernel<1, true>), g, dim3(256), 0, st, p);
-  else if (res_levels == 1) hipLaunchKernelGGL((assign_rescore_kernel<1, false>), g, dim3(256), 0, st, p);
-  else if (norm) hipLaunchKernelGGL((assign_rescore_kernel<2, true>), g, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((assign_rescore_kernel<2, false>), g, dim3(256), 0, st, p);
+  // two rows per wave for rows of <= 512 dims (RQSID_RESCORE_FULL=1: one row per wave, for A/B)
+  const char* ef = getenv("RQSID_RESCORE_FULL");
+  const bool half = dim <= kHalfDim && !(ef && atoi(ef));
+#define RQ_RS(RL, NORM)                                                                          \
+  do {                                                                                           \
+    if (half) hipLaunchKernelGGL((assign_rescore_half_kernel<RL, NORM>), g, dim3(256), 0, st, p); \
+    else hipLaunchKernelGGL((assign_rescore_kernel<RL, NORM>), g, dim3(256), 0, st, p);           \
+  } while (0)
+  if (res_levels == 0) RQ_RS(0, false);
+  else if (res_levels == 1 && norm) RQ_RS(1, true);
+  else if (res_levels == 1) RQ_RS(1, false);
+  else if (norm) RQ_RS(2, true);
+  else RQ_RS(2, false);
+#undef RQ_RS
   if ((rc = check_launch("assign_rescore"))) return rc;
   if (use_res) {
     // the resident screen's role waits are capped (assign_resident.hip): a wave that gave up waiting

@@ -516,3 +516,21 @@ def test_candidate_split_xl_levels_equal_multi_pass():
     ref = O.encode(xn[sel], [cb["c0"], cb["c1"], cb["c2"]], list(need), cb["match"], residual_from_weighted=True,
                    exact=True)
     assert (a[sel] == ref).all()
+
+
+@pytest.mark.parametrize("k,dim", [(300, 512), (64, 256), (200, 1024)])
+def test_rescore_two_rows_per_wave_equals_one(k, dim):
+    """The two-rows-per-wave re-score (rows of <= 512 dims) and the one-row form return the same IDs on
+    near-isotropic rows against many close centres (most rows listed, many overflowing to 'every
+    candidate'), an odd number of work items included; both equal the exact oracle."""
+    rng = np.random.default_rng(k + dim)
+    c = (rng.standard_normal((k, dim)) * 0.05 + 1.0).astype(np.float32)
+    x = (rng.standard_normal((4097, dim)) * 0.05 + 1.0).astype(np.float32)
+    pc = ops.prepare_centers(gpu(c))
+    ws = ops.AssignWorkspace(len(x), DEV)
+    a = ops.nearest(gpu(x), pc, workspace=ws, screen_terms=1).cpu().numpy()
+    assert ws.rescored() > 100
+    b = _with_env({"RQSID_RESCORE_FULL": 1}, lambda: ops.nearest(gpu(x), pc, screen_terms=1).cpu().numpy())
+    assert (a == b).all()
+    sel = np.arange(0, len(x), 7)
+    assert (a[sel] == exact_ids(x[sel], c)).all()

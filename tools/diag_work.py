@@ -29,7 +29,15 @@ def main(n=1_000_000, seed=99):
         ws = k.get("workspace")
         torch.cuda.synchronize()
         cnt = int(ws.buf[:4].view(torch.int32).item())
-        items = ws.buf[256:256 + 32 * cnt].view(torch.int32).view(cnt, 8).cpu().numpy()
+        nr = a[0].shape[0]
+        allw = ws.buf[256:256 + 32 * nr].view(torch.int32).view(nr, 8)
+        if lvl["i"] == 2 and os.environ.get("RQSID_SCREEN_VARIANT", "0") == "0":
+            # the ping-pong form stores items at work[row] and lists the rows in the compact-list area
+            off = 256 + 32 * nr + (nr * 4 + 255) // 256 * 256
+            idx = ws.buf[off:off + 4 * cnt].view(torch.int32).long()
+            items = allw[idx].cpu().numpy()
+        else:
+            items = allw[:cnt].cpu().numpy()
         ns = items[:, 2]
         vals, counts = np.unique(ns, return_counts=True)
         print(f"level {lvl['i']}: {cnt} items ({cnt / n:.2%}) " +
