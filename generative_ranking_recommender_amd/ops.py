@@ -86,8 +86,9 @@ class Buckets:
 def single_segment(n: int, device, rows_per_tile: Optional[int] = None) -> Buckets:
     """All n rows in one segment, identity order (layer 0 / dense prediction)."""
     tr = rows_per_tile or tile_rows()
-    off = torch.tensor([0, n], dtype=torch.int32, device=device)
-    toff = torch.tensor([0, (n + tr - 1) // tr], dtype=torch.int32, device=device)
+    # built by device fills, not host copies: the encode can be captured in a HIP graph
+    off = torch.arange(2, dtype=torch.int32, device=device) * n
+    toff = torch.arange(2, dtype=torch.int32, device=device) * ((n + tr - 1) // tr)
     return Buckets(off, toff, None, 1, (n + tr - 1) // tr)
 
 
