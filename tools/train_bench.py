@@ -8,6 +8,7 @@ import argparse
 import json
 import logging
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -39,8 +40,23 @@ def main():
     ap.add_argument("--sequential", action="store_true")
     ap.add_argument("--iter-limit", type=int, default=100)
     ap.add_argument("--out", default="")
+    ap.add_argument("--data", choices=("small", "bench"), default="small",
+                    help="small: synth.small_mixture (host); bench: bench.make_rows (the encode bench's rows, "
+                         "generated on the device, for 10M-row runs)")
     a = ap.parse_args()
-    x = synth.small_mixture(a.rows, m=4096, seed=5)
+    t_start = time.time()
+
+    def heartbeat():  # long phases log nothing for minutes; say the run is alive once a minute
+        while True:
+            time.sleep(60)
+            print(f"[heartbeat] {time.time() - t_start:.0f} s", flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
+    if a.data == "bench":
+        import bench  # noqa: E402  (tools/ run from the repo root)
+        x = bench.make_rows(a.rows, 0, torch.device("cuda", 0)).cpu().numpy()
+    else:
+        x = synth.small_mixture(a.rows, m=4096, seed=5)
     cfg = HierarchicalRQKMeansConfig(layer_clusters=[128, 1280, 1280], need_clusters=[128, 128, 256],
                                      embedding_dim=512, iter_limit=a.iter_limit)
     h = LayerTimes()
@@ -57,7 +73,8 @@ def main():
     total = time.time() - t
     ids = np.stack([r.cpu().numpy() for r in res["cluster_ids"]], 1)
     consistent = bool((model.predict(x, reference_quirks=False) == ids).all())
-    line = {"rows": a.rows, "mode": "sequential" if a.sequential else "lockstep", "total_s": round(total, 2),
+    line = {"rows": a.rows, "data": a.data, "mode": "sequential" if a.sequential else "lockstep",
+            "total_s": round(total, 2),
             "layers": [m for m in h.marks], "unique_ids": int(len(np.unique(ids, axis=0))),
             "train_encode_consistent": consistent}
     print(json.dumps(line), flush=True)
