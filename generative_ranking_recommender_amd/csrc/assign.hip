@@ -1308,11 +1308,12 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   const bool stream_ok = dim == 512 && cand_count_max <= 256 && !cand_lid && (res_levels != 1 || !norm || den_out) &&
                          n_rows >= 64 * 256 && (int64_t)n_segments + 1 <= n_rows &&
                          stream_supported(nt, t3, res_levels, norm);
-  // Default (variant 0): the ping-pong form for 1-term 256-candidate levels (measured L2 of the bench
-  // 7.58 vs 7.92 ms), the per-tile kernel elsewhere (L0 3.37 vs 3.99, L1 6.04 vs 6.54 ms).
+  // Default (variant 0): the ping-pong form for 1-term 256-candidate RESIDUAL levels (gathered rows;
+  // measured L2 of the bench 7.58 vs 7.92 ms), the per-tile kernel elsewhere (L0 3.37 vs 3.99, L1 6.04 vs
+  // 6.54 ms; the XL preset's 256-candidate level 0 on contiguous rows 3.03 vs 3.62-3.65 ms).
   // Variant 1 forces the per-tile kernel, variant 5 the stream forms (RQSID_STREAM_SHAPE).
   const int variant = screen_variant();
-  const int shape = variant == 5 ? 0 : (variant == 0 && nt == 8 && !t3 ? 88 : -1);
+  const int shape = variant == 5 ? 0 : (variant == 0 && nt == 8 && !t3 && res_levels >= 1 ? 88 : -1);
   const bool use_stream = stream_ok && shape >= 0 && variant != 6;
   // the centre-resident screen (assign_resident.hip): variant 6 forces it wherever it applies (1-term,
   // <= 256 candidates).  Not the default yet: measured L2 of the bench 8.0-9.1 ms against the ping-pong
