@@ -101,13 +101,63 @@ LEVEL_KERNELS = {
 PRESET = "prod"
 
 
-def level_traffic(path, lvl):
-    """HBM bytes (PMC FETCH_SIZE x2 + WRITE_SIZE) of one launch of level lvl's kernels, or None."""
+def level_traffic(path, lvl, rows):
+    """HBM bytes (PMC FETCH_SIZE x2 + WRITE_SIZE) of one launch of level lvl's kernels, or None -- also
+    when the counters were collected at another row count than this run's (they do not scale exactly)."""
     try:
-        ks = json.load(open(path))["kernels"]
+        d = json.load(open(path))
+        if int(d.get("rows") or -1) != int(rows):
+            return None
+        ks = d["kernels"]
         return sum(ks[k]["hbm_bytes"] for k in LEVEL_KERNELS[PRESET][lvl])
     except (OSError, KeyError, TypeError, ValueError):
         return None
+
+
+class SideWatchdog:
+    """The encode line is complete before the side measurements (train / balanced / parity / config0 /
+    CPU baseline) run, and those run collectives at N > 1.  If they take longer than ``budget`` seconds,
+    rank 0 prints the encode line as measured so far (marked ``side_measurements: stopped``) and every
+    rank exits with status 3 -- a hang is a failure the driver sees, while the line it needs is printed.
+    ``done(line)`` prints the full line instead (exactly one line either way)."""
+
+    EXIT_CODE = 3
+
+    def __init__(self, line: dict, budget: float, rank: int, exit_fn=os._exit):
+        self.line, self.budget, self.rank, self.exit_fn = line, budget, rank, exit_fn
+        self.printed, self.lock = threading.Event(), threading.Lock()
+        self.thread = threading.Thread(target=self._run, daemon=True)
+
+    def start(self):
+        self.thread.start()
+        return self
+
+    def _run(self):
+        if self.printed.wait(self.budget):
+            return
+        with self.lock:
+            if self.printed.is_set():
+                return
+            self.printed.set()
+            if self.rank == 0:
+                try:
+                    snap = dict(self.line)
+                    snap["side_measurements"] = f"stopped after {self.budget:.0f} s (watchdog; exit status {self.EXIT_CODE})"
+                    print(json.dumps(snap), flush=True)
+                except Exception:
+                    pass
+            sys.stdout.flush()
+            self.exit_fn(self.EXIT_CODE)
+
+    def done(self) -> bool:
+        """print the full line (rank 0); False when the watchdog already printed its snapshot"""
+        with self.lock:
+            if self.printed.is_set():
+                return False
+            if self.rank == 0:
+                print(json.dumps(self.line), flush=True)
+            self.printed.set()
+            return True
 
 
 class Timed:
@@ -237,13 +287,23 @@ def config0(dev, rows=100_000, cpu_rounds=40):
     gpu_s = time.perf_counter() - t
     km = m.trained_kmeans_models[0]
     iters = len(km.last_auction_rounds)
-    ids = np.array([m.semantic_ids[s][0] for s in sids[:4096]])
+    ids = np.array([m.semantic_ids[s][0] for s in sids])
+    # parity: every song's id is the exact nearest trained centre (the oracle on an evenly spaced sample)
+    # and the fit's balance is the reference's (:197: target 1.0 -> every cluster over-full, the min-loss
+    # choice falls on the latest iteration's centres)
+    c = km.cluster_centers.detach().cpu().numpy()
+    smp = np.linspace(0, rows - 1, 4096).astype(np.int64)
+    want = O.nearest(xs[smp], c, exact=True)
     out = {"workload": f"SimplifiedHierarchicalRQ.train, {rows} x {D}, layer_clusters = need_clusters = [128], "
                        f"iter_limit {cfg.iter_limit} (BASELINE configs[0])",
            "gpu": {"seconds": round(gpu_s, 2), "iterations": iters,
                    "auction_rounds": int(np.sum(km.last_auction_rounds)),
                    "s_per_iteration": round(gpu_s / max(iters, 1), 4),
-                   "ids_in_range": bool((ids >= 0).all() and (ids < 128).all())}}
+                   "ids_in_range": bool((ids >= 0).all() and (ids < 128).all())},
+           "parity": {"rows_checked": int(len(smp)), "mismatches": int((ids[smp] != want).sum()),
+                      "against": "oracle/rq_oracle.py nearest(exact=True) of the trained centres, evenly spaced rows",
+                      "cluster_sizes_min_max": [int(np.bincount(ids, minlength=128).min()),
+                                                int(np.bincount(ids, minlength=128).max())]}}
     # the CPU restatement of one iteration (the reference's own arithmetic, numpy)
     rng = np.random.default_rng(0)
     c = xs[rng.choice(rows, 128, replace=False)]
@@ -255,14 +315,15 @@ def config0(dev, rows=100_000, cpu_rounds=40):
     t = time.perf_counter()
     O.centroid_update(xs, a, c, lambda n: 0)
     t_u = time.perf_counter() - t
-    rounds = 1002 if rows % 128 else 13
+    rounds = int(round(out["gpu"]["auction_rounds"] / max(iters, 1)))  # the GPU fit's own rounds per iteration
     cpu_iter = t_d + rounds * t_r + t_u
     from threadpoolctl import threadpool_info
     threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
     out["cpu_baseline"] = {"value": round(cpu_iter, 2), "unit": "s per balanced Lloyd iteration", "cores": int(threads),
                            "kind": "port",
                            "sample": f"oracle/rq_oracle.py: cdist {t_d:.2f} s (numpy) + {cpu_rounds} auction rounds "
-                                     f"at {t_r * 1e3:.1f} ms (torch CPU ops, scaled to {rounds}) + update {t_u:.2f} s; "
+                                     f"at {t_r * 1e3:.1f} ms (torch CPU ops, scaled to the GPU fit's {rounds} rounds per "
+                                     f"iteration) + update {t_u:.2f} s; "
                                      f"{threads} BLAS threads, torch {torch.get_num_threads()} threads"}
     out["gpu_vs_cpu_per_iteration"] = round(cpu_iter / max(out["gpu"]["s_per_iteration"], 1e-9), 1)
     return out
@@ -493,7 +554,7 @@ def main():
         kern["bucket"] = {"ms": round(ms["bucket"], 3)}
     dom = max((k for k in kern if k.startswith("assign")), key=lambda k: kern[k]["ms"])
     dk = kern[dom]
-    traffic = level_traffic(args.traffic_json, int(dom[-1])) if os.environ.get("RQSID_SCREEN_VARIANT", "0") == "0" else None
+    traffic = level_traffic(args.traffic_json, int(dom[-1]), n) if os.environ.get("RQSID_SCREEN_VARIANT", "0") == "0" else None
     # Which roof applies: the level's algorithmic intensity (2 K_eff D flop per 2052 B: 64-128 flop/B) puts
     # its fp16 MFMA time at <= 6 % of its HBM time at the two peaks, so HBM is the roof; the PMC traffic
     # (when present) says whether the kernel moves more than its algorithmic bytes.
@@ -508,7 +569,8 @@ def main():
             "achieved": dk["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dk["hbm_frac"],
             "traffic": traffic, "traffic_unit": "bytes per launch",
             "traffic_source": (os.path.relpath(args.traffic_json, REPO) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
-                               "separate passes, same build and workload)") if traffic else None,
+                               "separate passes, same build and workload)") if traffic else
+                              "none: no PMC file for this build and row count",
             "algorithmic_bytes": n * bytes_row, "bytes_per_row": bytes_row}
 
     total_rows = n * world * args.steps
@@ -541,28 +603,8 @@ def main():
     if gather_ms is not None:
         line["gather_ids_ms"] = round(gather_ms, 3) if isinstance(gather_ms, float) else {"error": gather_ms}
     # The encode line is complete here.  The side measurements below run collectives at N > 1; a hang
-    # there must not cost the line: a watchdog prints what is measured so far and ends every rank.
-    printed, plock = threading.Event(), threading.Lock()
-
-    def watchdog():
-        budget = args.side_budget or (600.0 if world == 1 else 300.0)
-        if printed.wait(budget):
-            return
-        with plock:  # exactly one line: the main thread prints under the same lock
-            if printed.is_set():
-                return
-            printed.set()
-            if rank == 0:
-                try:
-                    snap = dict(line)
-                    snap["side_measurements"] = f"stopped after {budget:.0f} s (watchdog)"
-                    print(json.dumps(snap), flush=True)
-                except Exception:
-                    pass
-            sys.stdout.flush()
-            os._exit(0)
-
-    threading.Thread(target=watchdog, daemon=True).start()
+    # there must not cost the line (SideWatchdog).
+    dog = SideWatchdog(line, args.side_budget or (600.0 if world == 1 else 300.0), rank).start()
     if args.train_iters > 0:
         try:
             t_ms, rps = train_iterations(x, torch.from_numpy(cb["c0"]).to(dev).float(), args.train_iters, world,
@@ -587,12 +629,8 @@ def main():
             line["config0"] = config0(dev)
         except Exception as exc:  # a side measurement must not cost the encode line
             line["config0"] = {"error": repr(exc)[:300]}
-    with plock:
-        if printed.is_set():
-            return
-        if rank == 0:
-            print(json.dumps(line), flush=True)
-        printed.set()
+    if not dog.done():
+        return
     if dist:
         tdist.destroy_process_group()
 

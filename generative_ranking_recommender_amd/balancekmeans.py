@@ -15,6 +15,7 @@ moved to the GPU and the kernels raise if ``librqsid.so`` or the GPU is missing.
 """
 from __future__ import annotations
 
+import itertools
 import logging
 from typing import Optional
 
@@ -27,11 +28,15 @@ logger = logging.getLogger(__name__)
 
 # Step tracer for every K-Means fit of this module (tests certify each iteration against the oracle):
 # None, or a callable taking one dict per iteration.  KMeans.fit / fit_by_min_loss send
-# {"kind": "fit", "x", "half", "iteration", "centers_in", "scores" ([K][N] fp16 or None), "assign",
-# "centers_out"}; batched_fit sends {"kind": "batched", "x" (segment-ordered rows), "half", "iteration",
-# "active" (bool [S]), "off" (segment row offsets), "centers_in", "scores" (flat per-segment [K][N_s]
-# blocks or None), "assign" (local ids), "centers_out"}.
+# {"kind": "fit", "owner" (one number per KMeans object), "x", "half", "iteration", "centers_in", "scores"
+# ([K][N] fp16 or None), "assign", "centers_out", "loss"/"target" (fit_by_min_loss: the overflow loss of
+# centers_out, else None)}; batched_fit sends {"kind": "batched", "owner" (one number per fit_segments
+# call), "seg_base" (global index of the window's first segment), "window" (attempt number), "x"
+# (segment-ordered rows), "half", "iteration", "active" (bool [S]), "off" (segment row offsets),
+# "centers_in", "scores" (flat per-segment [K][N_s] blocks or None), "assign" (local ids), "centers_out",
+# "loss" (per segment, min-loss mode) / "target"}.
 TRACE = None
+_TRACE_OWNERS = itertools.count()
 
 
 def _device(device) -> torch.device:
@@ -103,6 +108,7 @@ class KMeans:
         self.balanced = balanced
         self.last_auction_rounds = []
         self.trace = TRACE  # per-iteration step tracer (see TRACE)
+        self._owner = next(_TRACE_OWNERS)
 
     # --- persistence (npz instead of the reference's pickle, :230-239) --------------------------
     @classmethod
@@ -141,11 +147,12 @@ class KMeans:
             return a
         return ops.nearest(X, ops.prepare_centers(self.cluster_centers))
 
-    def _emit(self, iteration: int, prev: torch.Tensor, a: torch.Tensor) -> None:
+    def _emit(self, iteration: int, prev: torch.Tensor, a: torch.Tensor, loss=None, target=None) -> None:
         if self.trace is not None:
-            self.trace({"kind": "fit", "x": self._x, "half": self._half, "iteration": iteration,
-                        "centers_in": prev.clone(), "scores": self._scores,
-                        "assign": a.clone(), "centers_out": self.cluster_centers.clone()})
+            self.trace({"kind": "fit", "owner": self._owner, "x": self._x, "half": self._half,
+                        "iteration": iteration, "centers_in": prev.clone(), "scores": self._scores,
+                        "assign": a.clone(), "centers_out": self.cluster_centers.clone(), "loss": loss,
+                        "target": target})
 
     def _update(self, X: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
         """:314-324 — per-cluster means; an empty cluster takes X[torch.randint(len(X), (1,))] (CPU RNG,
@@ -178,11 +185,10 @@ class KMeans:
                 self.cluster_centers = self.initialize(X)
             a = self._assign(X, half)
             prev = self._update(X, a)
-            self._emit(iteration, prev, a)
-            counts = torch.bincount(ops.nearest(X, ops.prepare_centers(self.cluster_centers)).long(),
-                                    minlength=self.n_clusters)
+            counts = torch.bincount(_loss_assign(X, self.cluster_centers, half), minlength=self.n_clusters)
             over = counts - target_nodes_num
             cur_loss = float(over[over > 0].sum().item()) if (over > 0).any() else 0
+            self._emit(iteration, prev, a, cur_loss, target_nodes_num)
             logger.debug("fit_by_min_loss: iteration %d loss %s", iteration, cur_loss)
             if cur_loss <= min_loss:
                 min_loss = cur_loss
@@ -236,6 +242,18 @@ class KMeans:
         return ids
 
 
+def _loss_assign(X: torch.Tensor, centers: torch.Tensor, half: bool) -> torch.Tensor:
+    """The nearest-centre assignment behind fit_by_min_loss's overflow loss (:327-329): the argmin of
+    ``pairwise_distance_function(X, C)``, i.e. of the fp32 distances (exact argmin here; the reference's
+    fp32 cdist can only differ on a near tie), or with ``half`` of the fp16 distances of
+    pairwise_distance_half, whose many EQUAL values make the first index matter: the fp16 scores
+    (rqsid_auction_scores, -distance) and their first maximum per row."""
+    if not half:
+        return ops.nearest(X, ops.prepare_centers(centers)).long()
+    w = ops.auction_scores(X, centers, half=True)  # [K][N] fp16 = -distance
+    return torch.argmax(w, dim=0)  # first index among equal values
+
+
 def init_indices(num_samples: int, n_clusters: int) -> np.ndarray:
     """The draw of KMeans.initialize (:240-256): np.random.choice over rows, with replacement only when
     K > N (global numpy RNG)."""
@@ -246,7 +264,7 @@ def init_indices(num_samples: int, n_clusters: int) -> np.ndarray:
 
 def batched_fit(X: torch.Tensor, layout: "ops.SegmentLayout", n_clusters: int, iter_limits, inits,
                 target_nodes_num=None, tol: float = 1e-3, half: bool = False, balanced: bool = True,
-                return_info: bool = False):
+                return_info: bool = False, trace_tag: Optional[dict] = None):
     """Many independent K-Means fits advanced in lockstep, one per segment of the segment-ordered rows X
     (segment s = rows layout.off[s] .. layout.off[s+1]), each exactly the iteration of KMeans.fit
     (:368-465; ``target_nodes_num`` None) or KMeans.fit_by_min_loss (:259-365; re-initialised every 10
@@ -319,16 +337,26 @@ def batched_fit(X: torch.Tensor, layout: "ops.SegmentLayout", n_clusters: int, i
         frozen = torch.from_numpy(~active).to(dev)
         new[frozen.repeat_interleave(K)] = prev[frozen.repeat_interleave(K)]
         centers = new.contiguous()
+        loss = None
+        if min_loss_mode:
+            if half:  # argmin of the fp16 distances, first index (:327-329 with pairwise_distance_half)
+                ws = ops.seg_auction_scores(X, centers, K, layout, half=True)
+                loc = torch.cat([ws[K * int(off[s]):K * int(off[s + 1])].view(K, -1).argmax(0)
+                                 for s in range(S)]) if layout.n else torch.zeros(0, dtype=torch.int64, device=dev)
+                glob = seg_row.long() * K + loc
+                del ws
+            else:
+                glob = ops.assign(X, ops.prepare_centers(centers), buckets, cand)[1].long()
+            hist = torch.bincount(glob, minlength=S * K).view(S, K)
+            loss = (hist - target_nodes_num).clamp(min=0).sum(1).cpu().numpy()
         if TRACE is not None:
             TRACE({"kind": "batched", "x": X, "half": half, "iteration": iteration.copy(), "active": active.copy(),
-                   "off": off.copy(),
-                   "centers_in": prev.clone(), "scores": w, "assign": a.clone(), "centers_out": centers.clone()})
+                   "off": off.copy(), "centers_in": prev.clone(), "scores": w, "assign": a.clone(),
+                   "centers_out": centers.clone(), "loss": None if loss is None else loss.copy(),
+                   "target": target_nodes_num, **(trace_tag or {"owner": -1, "seg_base": 0, "window": 0})})
         del w
         shift = torch.sqrt(torch.sum((centers - prev) ** 2, dim=1)).view(S, K).sum(1).cpu().numpy()
         if min_loss_mode:
-            glob = ops.assign(X, ops.prepare_centers(centers), buckets, cand)[1]
-            hist = torch.bincount(glob.long(), minlength=S * K).view(S, K)
-            loss = (hist - target_nodes_num).clamp(min=0).sum(1).cpu().numpy()
             better = active & (loss <= min_loss)
             if better.any():
                 min_loss[better] = loss[better]
@@ -396,9 +424,13 @@ def fit_segments(X: torch.Tensor, sizes, n_clusters: int, iter_limits, inits=Non
     centers = torch.empty((S * K, X.shape[1]), dtype=torch.float32, device=dev)
     last = torch.empty((max(X.shape[0], 1),), dtype=torch.int32, device=dev)
     torch_state = torch.get_rng_state()
-    start, restarts, guess = 0, 0, 0
+    owner, window = next(_TRACE_OWNERS), 0
+    start, restarts, guess, solo = 0, 0, 0, False
     while start < S:
-        stop = S if restarts <= max_restarts else start + 1
+        # after an attempt that kept nothing (the window's first segment drew out of the reference's order)
+        # that segment runs alone, which is exact by construction; the restart budget counts only attempts
+        # that made partial progress
+        stop = start + 1 if (solo or restarts > max_restarts) else S
         np_states, seg_inits = [], []
         for s in range(start, stop):
             if min_loss_mode:
@@ -417,7 +449,8 @@ def fit_segments(X: torch.Tensor, sizes, n_clusters: int, iter_limits, inits=Non
             layout = ops.SegmentLayout(sizes[m0:m1], dev)
             xs = X[int(off[m0]) - base:int(off[m1]) - base].contiguous()
             c_mine, a, info = batched_fit(xs, layout, K, limits[m0:m1], seg_inits[m0 - start:m1 - start],
-                                          target_nodes_num=target_nodes_num, tol=tol, half=half, return_info=True)
+                                          target_nodes_num=target_nodes_num, tol=tol, half=half, return_info=True,
+                                          trace_tag={"owner": owner, "seg_base": m0, "window": window})
             last[int(off[m0]) - base:int(off[m1]) - base] = a
             iters = np.asarray(info["iterations"], dtype=np.int64)
             ev = np.asarray([(m0 + e[0], guess + t) for t, e in enumerate(info["events"])],
@@ -457,7 +490,9 @@ def fit_segments(X: torch.Tensor, sizes, n_clusters: int, iter_limits, inits=Non
         torch_state = torch.get_rng_state()
         # next attempt: this rank's draws start after the lower ranks' draws of segments >= good
         guess = int(sum(int((e[:, 0] >= good).sum()) for r, e in enumerate(ev_all) if comm is not None and r < comm.rank))
-        if good < stop:
+        solo = good == start
+        if start < good < stop:
             restarts += 1
         start = good
+        window += 1
     return centers, last[:X.shape[0]]

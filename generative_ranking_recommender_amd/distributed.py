@@ -153,7 +153,10 @@ class ShardedLloyd:
             # balanced (KMeans(balanced=True), the reference's training): the row-sharded auction
             assign_fn = (lambda x, c: sharded_balanced_assign(x, c, n_global, half, group)) if balanced else _gpu_assign
         self.assign_fn = assign_fn
-        self.nearest_fn = nearest_fn or _gpu_assign
+        if nearest_fn is None:  # the min-loss histogram's assignment (balancekmeans._loss_assign: fp16 first argmin with half)
+            from .balancekmeans import _loss_assign
+            nearest_fn = lambda x, c: _loss_assign(x, c.float().contiguous(), half)  # noqa: E731
+        self.nearest_fn = nearest_fn
         self.accumulate_fn = accumulate_fn or _gpu_accumulate
         self.cluster_centers = None
 

@@ -271,6 +271,7 @@ class HierarchicalRQKMeans:
     def train(self, X: np.ndarray, resume: bool = True) -> Dict:
         """:368-537.  With a process group (``group=``) the rows are sharded across the ranks: see
         ``_train_sharded``."""
+        self.invalidate_encoder()
         if self.group is not None:
             return self._train_sharded(X, resume)
         cfg = self.config
@@ -821,11 +822,13 @@ class HierarchicalRQKMeans:
         return self.encode_shard(x, reference_quirks).cpu().numpy().astype(np.int64)
 
     def _encoder(self, reference_quirks: bool):
-        """The fused encoder of the trained codebooks (cached per semantics; rebuilt after training or
-        loading changes the codebooks)."""
+        """The fused encoder of the trained codebooks, cached per semantics.  The key holds each centre
+        tensor's identity and in-place version counter and each match matrix's identity, so assigning new
+        codebooks or changing a centre tensor in place rebuilds it; train / load_model drop the cache, and
+        ``invalidate_encoder`` does after an in-place edit of a numpy match matrix."""
         from .encode import LevelSemantics, RQEncoder
-        key = (bool(reference_quirks), len(self.cluster_centers_list), len(self.match_matrices),
-               tuple(id(c) for c in self.cluster_centers_list))
+        key = (bool(reference_quirks), tuple((id(c), getattr(c, "_version", 0)) for c in self.cluster_centers_list),
+               tuple(id(m) for m in self.match_matrices))
         cache = getattr(self, "_enc_cache", None)
         if cache is not None and cache[0] == key:
             return cache[1]
@@ -843,6 +846,10 @@ class HierarchicalRQKMeans:
                         group_dims=cfg.group_dims, weights=cfg.hierarchical_weights, semantics=sem, device=self.device)
         self._enc_cache = (key, enc)
         return enc
+
+    def invalidate_encoder(self) -> None:
+        """Drop the cached fused encoder (the next predict / encode_shard rebuilds it from the codebooks)."""
+        self._enc_cache = None
 
     def encode_shard(self, x: torch.Tensor, reference_quirks: bool = False) -> torch.Tensor:
         """Encode device-resident rows (this rank's shard): int32 [n, L] on the device.  The hot path of
@@ -873,6 +880,7 @@ class HierarchicalRQKMeans:
 
     def load_model(self, model_dir: str):
         """:1362-1391."""
+        self.invalidate_encoder()
         d = Path(model_dir)
         cf = d / "config.json"
         if cf.exists():

@@ -38,6 +38,18 @@ def cdist_f32(x: np.ndarray, c: np.ndarray) -> np.ndarray:
     return np.sqrt(np.maximum(d2, F32(0.0)), dtype=F32)
 
 
+def torch_cdist_batched(x: np.ndarray, c: np.ndarray, batch_size: int = 10000) -> np.ndarray:
+    """pairwise_distance_full (balancekmeans/__init__.py:576-603) itself: torch.cdist on the CPU over
+    batches of 10000 rows (the third-party arithmetic the reference calls; its summation order is that
+    of torch's CPU kernels, so on the host that produced the goldens it reproduces them bit for bit)."""
+    import torch
+    xt, ct = torch.from_numpy(np.ascontiguousarray(x, F32)), torch.from_numpy(np.ascontiguousarray(c, F32))
+    out = np.empty((len(x), len(c)), dtype=F32)
+    for i in range(0, len(x), batch_size):
+        out[i:i + batch_size] = torch.cdist(xt[i:i + batch_size].unsqueeze(0), ct.unsqueeze(0)).squeeze(0).numpy()
+    return out
+
+
 def cdist_half(x: np.ndarray, c: np.ndarray) -> np.ndarray:
     """pairwise_distance_half (balancekmeans/__init__.py:536-574): ``torch.cdist`` of the fp16-rounded
     operands, clamped at 1e-5, with torch's fp16 arithmetic (ATen ``_euclidean_dist`` on half tensors,
@@ -332,8 +344,7 @@ def auction_lap_half(job_and_worker_to_score: np.ndarray, tie_rule: str = "torch
             tv, ti = torch.from_numpy(value).topk(jpw + 1, dim=1)
             top_index = ti.numpy()
         else:
-            order = np.lexsort((np.arange(num_jobs)[None, :].repeat(num_workers, 0), -value.astype(F32)), axis=1)
-            top_index = order[:, :jpw + 1]
+            top_index = _stable_top(value, jpw + 1)
         top_values = np.take_along_axis(value, top_index, 1)
         inc = ((top_values[:, :-1].astype(F32) - top_values[:, -1:].astype(F32)).astype(np.float16).astype(F32)
                + F32(eps)).astype(np.float16)
@@ -354,6 +365,7 @@ def auction_lap_half(job_and_worker_to_score: np.ndarray, tie_rule: str = "torch
             high_bids = sub[high_bidders, np.arange(len(jobs_with_bidder))]
         if len(high_bidders) == num_jobs:
             return high_bidders.astype(np.int64)
+        prev = (cost.copy(), index)
         cost[jobs_with_bidder] = (cost[jobs_with_bidder].astype(F32) + high_bids.astype(F32)).astype(np.float16)
         value = (w.astype(F32) - cost[None, :].astype(F32)).astype(np.float16)
         index = high_bidders * num_jobs + jobs_with_bidder
@@ -361,6 +373,7 @@ def auction_lap_half(job_and_worker_to_score: np.ndarray, tie_rule: str = "torch
         counter += 1
         if max_rounds is not None and counter >= max_rounds:
             return None
+        counter = _fast_forward(counter, prev, cost, index, max_rounds)
 
 
 def auction_rounds_torch_cpu(job_and_worker_to_score: np.ndarray, rounds: int) -> float:
@@ -395,14 +408,43 @@ def auction_rounds_torch_cpu(job_and_worker_to_score: np.ndarray, rounds: int) -
     return (time.perf_counter() - t0) / rounds
 
 
+def _desc_key16(v16: np.ndarray) -> np.ndarray:
+    """uint16 keys whose ascending order is the DESCENDING order of fp16 values, with -0 == +0 (equal
+    values get equal keys, so a stable sort keeps the lowest index among them; 16-bit keys take numpy's
+    radix sort)."""
+    b = np.asarray(v16, np.float16).view(np.uint16)
+    b = np.where(b == 0x8000, np.uint16(0), b).astype(np.uint16)
+    asc = np.where(b & 0x8000, ~b, b | np.uint16(0x8000)).astype(np.uint16)
+    return (np.uint16(0xFFFF) - asc).astype(np.uint16)
+
+
+def _stable_top(value: np.ndarray, n: int) -> np.ndarray:
+    """indices of the n largest fp16 values per row, lowest index first among equal values"""
+    return np.argsort(_desc_key16(value), axis=1, kind="stable")[:, :n]
+
+
+def _fast_forward(counter: int, prev, cost: np.ndarray, index: np.ndarray, max_rounds=None) -> int:
+    """A round of auction_lap_half is a function of (cost, last winners ``index``, and which of the
+    counter's regimes it is in: retention bids while counter < 100, leftover bids once counter > 1000).
+    When a round left cost and winners unchanged (value is rebuilt from them), every later round of the
+    same regime repeats it, so the loop may jump to the regime's last round: the exact same result in
+    far fewer host rounds (the 1002-round runs of N % K != 0 spend most rounds waiting for round 1000)."""
+    if max_rounds is not None or prev[1] is None or not np.array_equal(prev[0], cost) \
+            or not np.array_equal(prev[1], index):
+        return counter
+    if counter < 100:          # rounds counter..99: retention bids, as the round just run
+        return 100
+    if 101 <= counter <= 1000:  # rounds counter..1000: neither retention nor leftover bids
+        return 1001
+    return counter
+
+
 def _auction_select(value: np.ndarray, jpw: int, tie_rule: str) -> np.ndarray:
     """top_index of ``value.topk(jpw + 1, dim=1)`` (balancekmeans/__init__.py:64-73) under a tie rule."""
     if tie_rule == "torch":
         import torch
         return torch.from_numpy(value).topk(jpw + 1, dim=1)[1].numpy()
-    num_workers, num_jobs = value.shape
-    order = np.lexsort((np.arange(num_jobs)[None, :].repeat(num_workers, 0), -value.astype(F32)), axis=1)
-    return order[:, :jpw + 1]
+    return _stable_top(value, jpw + 1)
 
 
 def _auction_max(sub: np.ndarray, tie_rule: str):
@@ -475,11 +517,12 @@ def auction_tie_certificate(job_and_worker_to_score: np.ndarray) -> dict:
         if len(hbr) == num_jobs:
             out["torch"] = out["stable"] = hbr.astype(np.int64)
             return out
+        prev = (cost.copy(), index)
         cost[jobs_with_bidder] = (cost[jobs_with_bidder].astype(F32) + hb.astype(F32)).astype(np.float16)
         value = (w.astype(F32) - cost[None, :].astype(F32)).astype(np.float16)
         index = hbr * num_jobs + jobs_with_bidder
         value.reshape(-1)[index] = w.reshape(-1)[index]
-        counter += 1
+        counter = _fast_forward(counter + 1, prev, cost, index)
 
 
 def assignment_quality(job_and_worker_to_score: np.ndarray, assign: np.ndarray) -> dict:
@@ -558,9 +601,12 @@ class LegacyRNG:
 
 
 def kmeans_fit(x: np.ndarray, k: int, rng: LegacyRNG, iter_limit: int, balanced: bool, tol: float = 1e-3,
-               min_loss_target: Optional[float] = None):
+               min_loss_target: Optional[float] = None, dist_fn=None):
     """KMeans.fit (balancekmeans/__init__.py:368-465) and, with min_loss_target, KMeans.fit_by_min_loss
-    (:259-365).  Returns (centers, last assignment)."""
+    (:259-365).  Returns (centers, last assignment).  ``dist_fn`` replaces the fp32 distance (default
+    ``cdist_f32``; ``torch_cdist_batched`` is the reference's own torch.cdist call, bit for bit on the
+    same host)."""
+    cdist_f32 = dist_fn or globals()["cdist_f32"]
     x = x.astype(F32)
     c = x[rng.choice(len(x), k)].copy()
     it = 0
@@ -582,6 +628,131 @@ def kmeans_fit(x: np.ndarray, k: int, rng: LegacyRNG, iter_limit: int, balanced:
         if shift ** 2 < tol or (iter_limit != 0 and it >= iter_limit):
             break
     return (best_c if min_loss_target is not None else c), a
+
+
+# ---------------------------------------------------------------------------
+# last-layer match matrix (hierarchical :968-1053, simplified :247-303)
+# ---------------------------------------------------------------------------
+def greedy_unique_nearest(sub: np.ndarray, cand: np.ndarray, n_take: int, dist: str = "cdist") -> List[int]:
+    """The greedy step of the match-matrix builders: sub-centre j (in order) takes its nearest candidate
+    not taken yet.  ``dist="cdist"``: hierarchical_rq_kmeans.py:1024-1036 (fp32 torch.cdist, the used
+    columns set to inf, torch.argmin = first index); ``dist="norm"``: simplified…:279-291 (fp32
+    np.linalg.norm of the differences, argsort, first unused; the sort's order among EQUAL distances is
+    unspecified in the reference, lowest index here).  Returns the taken columns in pick order."""
+    if dist == "cdist":
+        d = cdist_f32(sub, cand)
+    else:
+        d = np.linalg.norm(sub.astype(F32)[:, None, :] - cand.astype(F32)[None, :, :], axis=2)
+    used: List[int] = []
+    for j in range(n_take):
+        row = d[j].astype(F32).copy()
+        if used:
+            row[used] = np.inf
+        used.append(int(np.argmin(row)))  # first index among equal values (argsort(kind=stable) agrees)
+    return used
+
+
+def greedy_certificate(sub: np.ndarray, cand: np.ndarray, n_take: int) -> dict:
+    """Which columns EVERY correct fp32 implementation of the greedy step must take.  Distances are
+    exact (fp64) with the bound of any fp32 summation order of either distance form (torch.cdist's
+    mm expansion or the norm of the differences) plus the final sqrt rounding; step j is determined when
+    the exact nearest unused column's upper bound is below every other unused column's lower bound.
+    Returns {"determined": all steps determined, "step": first undetermined step (or n_take), "taken":
+    the determined columns in order, "tied": the columns that could win the undetermined step}."""
+    s = np.asarray(sub, F32).astype(np.float64)
+    c = np.asarray(cand, F32).astype(np.float64)
+    sn, cn = (s * s).sum(1), (c * c).sum(1)
+    d2 = sn[:, None] + cn[None, :] - 2.0 * (s @ c.T)
+    e = _fp32_sum_bound(s.shape[1] + 2) * (2.0 * (np.abs(s) @ np.abs(c).T) + sn[:, None] + cn[None, :]) * 2.0
+    e = e + 2.0 ** -21 * np.abs(d2)
+    taken: List[int] = []
+    free = np.ones(len(c), bool)
+    for j in range(n_take):
+        dj = np.where(free, d2[j], np.inf)
+        m = int(np.argmin(dj))
+        rivals = free & (d2[j] - e[j] <= d2[j, m] + e[j, m])
+        rivals[m] = False
+        if rivals.any():
+            return {"determined": False, "step": j, "taken": taken, "tied": sorted([m] + np.nonzero(rivals)[0].tolist())}
+        taken.append(m)
+        free[m] = False
+    return {"determined": True, "step": n_take, "taken": taken, "tied": []}
+
+
+def assign_last_match_matrix(x: np.ndarray, l1: np.ndarray, l2: np.ndarray, cand: np.ndarray,
+                             prev_prev_need: int, prev_need: int, need: int, trunc: int, fit_fn,
+                             subs_out: Optional[list] = None) -> np.ndarray:
+    """HierarchicalRQKMeans._assign_last_match_matrix (hierarchical_rq_kmeans.py:968-1053) on the global
+    numpy RNG: per (l1, l2) group in order — no rows: all-zero row (:999-1001); <= need rows: the rows
+    (:1005-1006); < trunc rows: ``np.random.choice(n, need, replace=False)`` of them (:1007-1010); else
+    ``fit_fn(rows)`` (the balanced sub-K-Means, :1011-1018; it must draw its own initialisation); the
+    greedy step (:1020-1036); the random fill (:1042-1049).  ``subs_out`` collects each non-empty group's
+    greedy operand."""
+    n_cand = len(cand)
+    out = np.zeros((prev_prev_need * prev_need, n_cand), dtype=np.uint8)
+    for i in range(prev_prev_need):
+        for j in range(prev_need):
+            idx = np.nonzero((l1 == i) & (l2 == j))[0]
+            if len(idx) == 0:
+                continue
+            sub = x[idx]
+            if len(idx) <= need:
+                centers = sub
+            elif len(idx) < trunc:
+                centers = sub[np.random.choice(len(idx), need, replace=False)]
+            else:
+                centers = fit_fn(sub)
+            if subs_out is not None:
+                subs_out.append(np.asarray(centers, F32))
+            taken = set(greedy_unique_nearest(centers, cand, min(len(centers), need), "cdist"))
+            if len(taken) < need:
+                for _ in range(need - len(taken)):
+                    r = np.random.randint(n_cand)
+                    while r in taken:
+                        r = np.random.randint(n_cand)
+                    taken.add(r)
+            out[i * prev_need + j, sorted(taken)] = 1
+    return out
+
+
+def dynamic_match_matrix(x: np.ndarray, l1: np.ndarray, l2: np.ndarray, cand: np.ndarray, n_prev1: int,
+                         n_prev2: int, need: int, fit_fn, subs_out: Optional[list] = None) -> np.ndarray:
+    """SimplifiedHierarchicalRQ._get_dynamic_match_matrix (simplified_semantic_id_generator.py:247-303):
+    per (l1, l2) group — no rows: ``need`` candidates drawn with np.random.choice(replace=False) (:267-268);
+    <= need rows: the rows (:269-270); else ``fit_fn(rows)`` (``fit(iter_limit=20)``, :271-276); the greedy
+    step over every sub-centre (:279-291); the fill ``while len < need: randint`` (:293-296)."""
+    n_cand = len(cand)
+    out = np.zeros((n_prev1 * n_prev2, n_cand), dtype=np.uint8)
+    for i in range(n_prev1):
+        for j in range(n_prev2):
+            idx = np.nonzero((l1 == i) & (l2 == j))[0]
+            if len(idx) == 0:
+                centers = cand[np.random.choice(n_cand, need, replace=False)]
+            elif len(idx) <= need:
+                centers = x[idx]
+            else:
+                centers = fit_fn(x[idx])
+            if subs_out is not None:
+                subs_out.append(np.asarray(centers, F32))
+            taken = set(greedy_unique_nearest(centers, cand, len(centers), "norm"))
+            while len(taken) < need:
+                r = np.random.randint(n_cand)
+                if r not in taken:
+                    taken.add(r)
+            out[i * n_prev2 + j, sorted(taken)] = 1
+    return out
+
+
+def recorded_fits(centres: Sequence[np.ndarray], k: int):
+    """A ``fit_fn`` for the builders above that replays recorded sub-K-Means results: it draws the fit's
+    initialisation (KMeans.initialize, balancekmeans/__init__.py:240-256; a balanced fit of N >= K rows
+    draws nothing else from numpy) and returns the next recorded centres."""
+    it = iter(centres)
+
+    def fit(rows):
+        np.random.choice(len(rows), k, replace=k > len(rows))
+        return next(it)
+    return fit
 
 
 def adaptive_iter_limit(num_samples: int, n_clusters: int, layer: int, base_iter_limit: int = 100,

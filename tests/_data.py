@@ -62,6 +62,43 @@ def prod_encode_inputs(g):
     return x, cb
 
 
+MATCH_SIZES = [0, 3, 8, 12, 15, 16, 40, 0, 5, 9, 64, 1, 20, 33, 7, 100]  # rows per (l1, l2) group, 4 x 4
+MATCH_NEED = [4, 4, 8]
+MATCH_CAND = 64
+
+
+def match_inputs(g=None):
+    """tests/golden/make_golden.py g_match: rows of 16 (l1, l2) groups of every kind the match-matrix
+    builders distinguish (empty, fewer than / exactly need rows, fewer than 2*need rows, fitted; N % K
+    zero and non-zero), in shuffled row order, and 64 candidate centres from the same mixture with one
+    exact duplicate (candidate 63 = candidate 5)."""
+    n = sum(MATCH_SIZES)
+    xa = synth.small_mixture(n + MATCH_CAND, m=24, seed=51)
+    xa /= np.linalg.norm(xa, axis=1, keepdims=True)
+    xa = xa.astype(np.float32)
+    x, cand = xa[:n].copy(), xa[n:].copy()
+    cand[63] = cand[5]
+    gid = np.repeat(np.arange(len(MATCH_SIZES)), MATCH_SIZES)
+    np.random.default_rng(52).shuffle(gid)
+    l1, l2 = gid // MATCH_NEED[1], gid % MATCH_NEED[1]
+    if g is not None:
+        checked(x, g["x_sha"])
+        checked(cand, g["cand_sha"])
+    return x, l1.astype(np.int64), l2.astype(np.int64), cand
+
+
+CONFIG0_CASES = {"k8": (2050, 8, 5, 61), "k128": (12800, 128, 3, 62)}  # rows, K, iter_limit, data seed
+
+
+def config0_inputs(tag, g=None):
+    """BASELINE configs[0]'s single-level simplified run at golden size (make_golden.py g_config0)."""
+    n, k, it, seed = CONFIG0_CASES[tag]
+    x = synth.small_mixture(n, m=max(2 * k, 64), seed=seed)
+    if g is not None:
+        checked(x, g[f"{tag}_x_sha"])
+    return x, k, it
+
+
 def half_inputs(g):
     """tests/golden/make_golden.py half_inputs (pairwise_distance_half fixture)."""
     x = synth.small_mixture(640, m=32, seed=41)

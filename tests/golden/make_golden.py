@@ -333,6 +333,125 @@ def g_encode_prod():
          pred_train=pred_train.astype(np.int64))
 
 
+# --- G-match: the last layer's match-matrix builders, called directly ----------
+def _rng_after():
+    """the next draws of both global generators (pins the RNG state the builder leaves behind)"""
+    return np.random.randint(1 << 30, size=4).astype(np.int64), torch.randint(1 << 30, (4,)).numpy().astype(np.int64)
+
+
+def g_match():
+    """HierarchicalRQKMeans._assign_last_match_matrix (:968-1053) and
+    SimplifiedHierarchicalRQ._get_dynamic_match_matrix (simplified…:247-303) on fixed inputs
+    (tests/_data.match_inputs: 16 groups of every kind).  Besides each returned matrix the capture
+    records every group's sub-centres exactly as the reference computed them (the operand of its greedy
+    step), the fitted sub-K-Means centres, and the next draws of the numpy / torch generators."""
+    from tests import _data
+    x, l1, l2, cand = _data.match_inputs()
+    need = _data.MATCH_NEED
+    cfg = ref_h.HierarchicalRQKMeansConfig(layer_clusters=[4, 16, 32], need_clusters=list(need), embedding_dim=512)
+    cand_t = torch.from_numpy(cand)
+    fitted = []
+
+    class RecKMeans(ref_bk.KMeans):
+        def fit(self, *a, **kw):
+            out = super().fit(*a, **kw)
+            fitted.append(self.cluster_centers.detach().cpu().numpy().copy())
+            return out
+
+    # hierarchical: the greedy operand is the first argument of torch.cdist(sub_centers, candidates) (:1027)
+    subs_h = []
+    orig_cdist = torch.cdist
+
+    def cdist_rec(a, b, *args, **kw):
+        if b.data_ptr() == cand_t.data_ptr():
+            subs_h.append(a.detach().numpy().copy())
+        return orig_cdist(a, b, *args, **kw)
+
+    m = ref_h.HierarchicalRQKMeans(cfg, device=torch.device("cpu"))
+    seed_all(71)
+    ref_h.KMeans, torch.cdist = RecKMeans, cdist_rec
+    try:
+        match_h = m._assign_last_match_matrix(cand_t, 2 * 32, torch.from_numpy(x), need[0], need[1], l1, l2,
+                                              need[2], 2 * need[2], 2)
+    finally:
+        ref_h.KMeans, torch.cdist = ref_bk.KMeans, orig_cdist
+    h_np, h_torch = _rng_after()
+    fitted_h, fitted[:] = list(fitted), []
+    # simplified: the greedy operand is rebuilt from the recorded draws (empty group -> its candidate
+    # sample, :268; <= need rows -> the rows, :270; else the fitted centres, :276)
+    choices = []
+    orig_choice = np.random.choice
+
+    def choice_rec(*a, **kw):
+        r = orig_choice(*a, **kw)
+        choices.append(np.asarray(r).copy())
+        return r
+
+    s = ref_s.SimplifiedHierarchicalRQ.__new__(ref_s.SimplifiedHierarchicalRQ)
+    s.config, s.device = cfg, torch.device("cpu")
+    seed_all(72)
+    ref_s.KMeans, np.random.choice = RecKMeans, choice_rec
+    try:
+        match_s = s._get_dynamic_match_matrix(torch.from_numpy(x), torch.from_numpy(l1), torch.from_numpy(l2), cand_t)
+    finally:
+        ref_s.KMeans, np.random.choice = ref_bk.KMeans, orig_choice
+    s_np, s_torch = _rng_after()
+    gid = l1 * need[1] + l2
+    subs_s, ci, fi = [], 0, 0
+    for g in range(need[0] * need[1]):
+        rows = np.nonzero(gid == g)[0]
+        if len(rows) == 0:
+            subs_s.append(cand[choices[ci]])
+            ci += 1
+        elif len(rows) <= need[2]:
+            subs_s.append(x[rows])
+        else:
+            subs_s.append(fitted[fi])
+            ci += 1  # the fit's KMeans.initialize draw
+            fi += 1
+    assert ci == len(choices) and fi == len(fitted)
+
+    def cat(parts):
+        return (np.concatenate(parts, 0).astype(np.float32),
+                np.concatenate([[0], np.cumsum([len(p) for p in parts])]).astype(np.int64))
+    sh, sh_off = cat(subs_h)
+    ss, ss_off = cat(subs_s)
+    fh, fh_off = cat(fitted_h) if fitted_h else (np.zeros((0, 512), np.float32), np.zeros(1, np.int64))
+    save("match", x_sha=np.array(synth.sha256(x)), cand_sha=np.array(synth.sha256(cand)),
+         hier_match=np.array(match_h, dtype=np.uint8), hier_sub=sh, hier_sub_off=sh_off,
+         hier_fitted=fh, hier_fitted_off=fh_off, hier_np_after=h_np, hier_torch_after=h_torch,
+         simp_match=match_s.numpy().astype(np.uint8), simp_sub=ss, simp_sub_off=ss_off,
+         simp_np_after=s_np, simp_torch_after=s_torch)
+
+
+# --- G-config0: BASELINE configs[0], the single-level simplified run (L = 1) -----
+def g_config0():
+    """SimplifiedHierarchicalRQ.train with layer_clusters = need_clusters = [K] (simplified…:176-245):
+    one balanced fit_by_min_loss with target_nodes_num = np.prod([]) = 1.0 (:197), then predict.  Two
+    golden-size cases (tests/_data.CONFIG0_CASES): K = 8 with N % K != 0 (1002-round auctions) and the
+    configs[0] K = 128."""
+    from tests import _data
+    out = {}
+    for tag in _data.CONFIG0_CASES:
+        x, k, it = _data.config0_inputs(tag)
+        sids = [f"s{i:05d}" for i in range(len(x))]
+        with tempfile.TemporaryDirectory() as td:
+            p = os.path.join(td, "vec.csv")
+            write_csv(p, sids, x)
+            seed_all(42)
+            model = ref_s.SimplifiedHierarchicalRQ(ref_h.HierarchicalRQKMeansConfig(
+                layer_clusters=[k], need_clusters=[k], embedding_dim=512, iter_limit=it))
+            model.train(p)
+            o = os.path.join(td, "ids.jsonl")
+            model.save_semantic_ids(o)
+            raw = Path(o).read_bytes()
+        out[f"{tag}_x_sha"] = np.array(synth.sha256(x))
+        out[f"{tag}_ids"] = np.array([model.semantic_ids[s] for s in sids], dtype=np.int64)
+        out[f"{tag}_centers"] = model.trained_kmeans_models[0].cluster_centers.numpy()
+        out[f"{tag}_jsonl_sha"] = np.array(synth.sha256(np.frombuffer(raw, dtype=np.uint8)))
+    save("config0", **out)
+
+
 # --- G-csv: loader skip rules (simplified :38-76) ----------------------------
 def g_csv():
     rows = [["a", "1", "2", "3", "4"], ["b"], ["c", "1", "x", "3", "4"], ["d", "1", "2", "3"],
@@ -354,6 +473,6 @@ def g_csv():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["assign", "residual", "update", "auction", "fit", "simplified",
-                             "hierarchical", "encode_prod", "csv", "dist_half", "trainer"]
+                             "hierarchical", "encode_prod", "csv", "dist_half", "trainer", "match", "config0"]
     for w in which:
         globals()[f"g_{w}"]()

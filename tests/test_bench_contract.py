@@ -23,3 +23,34 @@ def test_level_kernels_match_committed_traffic():
         for lvl, ks in lk[preset].items():
             missing = [k for k in ks if k not in names]
             assert not missing, f"{preset} level {lvl}: {missing} not in {path}"
+
+
+def test_side_watchdog_prints_the_encode_line_and_exits_nonzero(capsys):
+    """a hang in the side measurements after the timed region ends with the encode line
+    printed (marked stopped) and a NON-ZERO exit status, so the driver sees the failure."""
+    import sys
+    import time
+    sys.path.insert(0, str(REPO))
+    import bench
+    codes = []
+    line = {"metric": "vectors quantized/sec (3-level RQ, 512-d)", "value": 1.0}
+    dog = bench.SideWatchdog(line, 0.05, rank=0, exit_fn=codes.append).start()
+    dog.thread.join(5)
+    assert codes == [bench.SideWatchdog.EXIT_CODE] and codes[0] != 0
+    out = capsys.readouterr().out.strip().splitlines()
+    assert len(out) == 1
+    got = json.loads(out[0])
+    assert got["value"] == 1.0 and got["side_measurements"].startswith("stopped")
+    assert dog.done() is False  # the main thread's late print is suppressed: one line only
+    assert capsys.readouterr().out == ""
+
+
+def test_side_watchdog_quiet_when_done_in_time(capsys):
+    import sys
+    sys.path.insert(0, str(REPO))
+    import bench
+    codes = []
+    dog = bench.SideWatchdog({"value": 2.0}, 30.0, rank=0, exit_fn=codes.append).start()
+    assert dog.done() is True
+    dog.thread.join(5)
+    assert codes == [] and json.loads(capsys.readouterr().out)["value"] == 2.0

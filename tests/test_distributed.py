@@ -279,7 +279,7 @@ def test_sharded_auction_matches_single_process(world, n, k, levels):
 
 # ---- segment-parallel sub-fits: the exact-RNG machinery of balancekmeans.fit_segments ----------------
 def _stub_batched_fit(X, layout, n_clusters, iter_limits, inits, target_nodes_num=None, tol=1e-3, half=False,
-                      balanced=True, return_info=False):
+                      balanced=True, return_info=False, trace_tag=None):
     """A CPU stand-in for the lockstep GPU loop with its RNG behaviour: segment s converges after
     ``1 + size % 13`` iterations (early, before its budget, for most sizes), re-initialises from
     inits[s][it // 10] at iterations 10, 20, ... (min-loss mode), and has 'empty clusters' (one
@@ -350,6 +350,34 @@ def _fs_worker(rank, world, port, sizes, k, limits, target, seed, out):
                            max_restarts=2)
     out.put((rank, c.numpy(), np.random.get_state()[1].copy(), torch.get_rng_state().numpy().copy()))
     dist.destroy_process_group()
+
+
+def test_fit_segments_progresses_when_the_first_segment_draws_out_of_order(monkeypatch):
+    """when the first torch draw out of the reference's order belongs to the window's FIRST
+    segment (segment 1 draws at iteration 0, segment 0 only at iteration 2), an attempt keeps nothing; the
+    next attempt runs that segment alone (exact by construction) and then widens again, without charging
+    the restart budget: 3 lockstep runs here (full, solo, rest), results and generator states equal to the
+    reference's one-after-another loop."""
+    import generative_ranking_recommender_amd.balancekmeans as bk
+    calls = []
+
+    def counting(*a, **kw):
+        calls.append(a[1].n_seg)
+        return _stub_batched_fit(*a, **kw)
+    monkeypatch.setattr(bk, "batched_fit", counting)
+    sizes = np.array([4, 3], dtype=np.int64)  # stub draws: segment 0 at iteration 2, segment 1 at 0 and 3
+    k = 4
+    np.random.seed(5)
+    torch.manual_seed(5)
+    inits = [[bk.init_indices(int(n), k)] for n in sizes]
+    c, _ = bk.fit_segments(torch.zeros((int(sizes.sum()), 2)), sizes, k, [6, 6], inits, max_restarts=3)
+    t_state = torch.get_rng_state()
+    assert calls == [2, 1, 1]
+    np.random.seed(5)
+    torch.manual_seed(5)
+    inits2 = [[bk.init_indices(int(n), k)] for n in sizes]
+    want = _stub_reference(sizes, k, [6, 6], lambda s: inits2[s], None)
+    assert torch.equal(c, want) and torch.equal(t_state, torch.get_rng_state())
 
 
 @pytest.mark.parametrize("world,target", [(2, 5), (3, 5), (2, None)])

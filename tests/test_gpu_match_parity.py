@@ -1,0 +1,159 @@
+"""The last layer's match-matrix builders on the GPU against the REFERENCE's own outputs (SURVEY §8f row 2,
+VERDICT r3 "What's missing" #1): tests/golden/match.npz holds what the reference's
+HierarchicalRQKMeans._assign_last_match_matrix (hierarchical_rq_kmeans.py:968-1053) and
+SimplifiedHierarchicalRQ._get_dynamic_match_matrix (simplified_semantic_id_generator.py:247-303) returned
+when called directly on fixed rows, previous-level ids and candidates (tests/_data.match_inputs: 16 groups
+of every kind), plus every group's greedy operand and the generators' next draws.
+
+Two checks per builder:
+1. the greedy kernel (rqsid_greedy_match on rqsid_pairwise_distance) on the reference's own operands takes
+   every column the certificate O.greedy_certificate proves any correct fp32 implementation must take;
+2. the whole GPU builder with the reference's seeds reproduces the reference's rows group by group: a
+   group is required to be identical unless a certified divergence explains it (its sub-K-Means took a
+   certified divergence, tests/_certify.py, or its greedy step is an fp32 near tie), and while no
+   difference has touched the random draws the generators end where the reference's did.
+"""
+import numpy as np
+import pytest
+import torch
+
+from generative_ranking_recommender_amd import ops
+from generative_ranking_recommender_amd.hierarchical_rq_kmeans import HierarchicalRQKMeans, HierarchicalRQKMeansConfig
+from generative_ranking_recommender_amd.simplified_semantic_id_generator import SimplifiedHierarchicalRQ
+from generative_ranking_recommender_amd import balancekmeans as bk
+from oracle import rq_oracle as O
+from tests import _certify, _data
+from tests.test_gpu_reference_parity import report, seeded
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+NEED = _data.MATCH_NEED
+SIZES = np.asarray(_data.MATCH_SIZES)
+CFG = dict(layer_clusters=[4, 16, 32], need_clusters=list(NEED), embedding_dim=512)
+
+
+@pytest.fixture
+def tracer():
+    rec = _certify.Recorder()
+    bk.TRACE = rec
+    try:
+        yield rec
+    finally:
+        bk.TRACE = None
+
+
+def _operands(g, variant):
+    sub, off = g[f"{variant}_sub"], g[f"{variant}_sub_off"]
+    groups = [i for i, n in enumerate(SIZES) if n > 0] if variant == "hier" else list(range(len(SIZES)))
+    return {gi: sub[off[k]:off[k + 1]] for k, gi in enumerate(groups)}
+
+
+@pytest.mark.parametrize("variant", ["hier", "simp"])
+def test_greedy_kernel_on_reference_operands(golden, variant):
+    g = golden("match")
+    _, _, _, cand = _data.match_inputs(g)
+    ops_by_group = _operands(g, variant)
+    groups = sorted(ops_by_group)
+    takes = [min(len(ops_by_group[gi]), NEED[2]) for gi in groups]
+    sc = np.concatenate([ops_by_group[gi][:t] for gi, t in zip(groups, takes)], 0)
+    sub_off = torch.tensor(np.concatenate([[0], np.cumsum(takes)]), dtype=torch.int32, device=DEV)
+    c_t = torch.from_numpy(cand).to(DEV)
+    rows, nsel = ops.greedy_match(ops.pairwise_distance(torch.from_numpy(sc).to(DEV), c_t), sub_off, NEED[2])
+    rows = rows.cpu().numpy()
+    undetermined = 0
+    for i, gi in enumerate(groups):
+        cert = O.greedy_certificate(ops_by_group[gi], cand, takes[i])
+        got = set(np.nonzero(rows[i])[0].tolist())
+        ref_row = g[f"{variant}_match"][gi]
+        assert set(cert["taken"]) <= got
+        if cert["determined"]:
+            assert got == set(cert["taken"]), (gi, got, cert)
+            assert ref_row[sorted(got)].all()  # the reference took the same columns (plus its random fill)
+        else:
+            undetermined += 1
+            assert len(got) == takes[i]
+    report("greedy_on_reference_operands", variant=variant, groups=len(groups), undetermined=undetermined)
+
+
+def _compare_builder(g, variant, got, fitted_groups, diverged, np_after, torch_after):
+    """group-by-group comparison of a GPU builder's matrix with the reference's (rules in the module doc)"""
+    ref = g[f"{variant}_match"]
+    ops_by_group = _operands(g, variant)
+    _, _, _, cand = _data.match_inputs(g)
+    sync, excused, identical = True, [], 0
+    for gi in range(len(SIZES)):
+        n = int(SIZES[gi])
+        if variant == "hier" and n == 0:
+            assert not got[gi].any() and not ref[gi].any()  # empty group -> all-zero row (:999-1001)
+            continue
+        fit_div = gi in fitted_groups and fitted_groups.index(gi) in diverged
+        op = ops_by_group[gi]
+        take = min(len(op), NEED[2])
+        cert = O.greedy_certificate(op, cand, take)
+        expect_exact = sync and not fit_div and cert["determined"]
+        same = bool(np.array_equal(got[gi], ref[gi]))
+        if expect_exact:
+            assert same, f"group {gi} ({n} rows) differs from the reference without a certified divergence"
+        identical += same
+        if not same:
+            excused.append((gi, "fit" if fit_div else "greedy" if not cert["determined"] else "rng"))
+            if take < NEED[2]:
+                sync = False  # its random fill may have drawn differently from here on
+        assert got[gi].sum() == NEED[2]
+    if sync:
+        assert np.array_equal(np_after, g[f"{variant}_np_after"]), "numpy generator state differs from the reference"
+        assert np.array_equal(torch_after, g[f"{variant}_torch_after"]), "torch generator state differs"
+    return identical, excused, sync
+
+
+def test_hierarchical_match_matrix_matches_reference(golden, tracer):
+    g = golden("match")
+    x, l1, l2, cand = _data.match_inputs(g)
+    m = HierarchicalRQKMeans(HierarchicalRQKMeansConfig(**CFG), device=DEV)
+    seeded(71)
+    got = m._assign_last_match_matrix(torch.from_numpy(cand).to(DEV), 2 * 32, torch.from_numpy(x).to(DEV), NEED[0],
+                                      NEED[1], torch.from_numpy(l1), torch.from_numpy(l2), NEED[2], 2 * NEED[2], 2)
+    np_after, torch_after = np.random.randint(1 << 30, size=4), torch.randint(1 << 30, (4,)).numpy()
+    st = _certify.certify_trace(tracer.events)
+    owners = _certify.owners(tracer.events, "batched")
+    assert len(owners) == 1
+    fitted = [gi for gi, n in enumerate(SIZES) if n >= 2 * NEED[2]]
+    diverged = _certify.diverged_segments(st, owners[0])
+    identical, excused, sync = _compare_builder(g, "hier", np.asarray(got), fitted, diverged, np_after, torch_after)
+    report("hier_match_matrix", identical_rows=identical, excused=excused, rng_in_sync=sync, fitted=len(fitted),
+           diverged_fits=sorted(diverged), **{k: v for k, v in st.items() if k != "segments"})
+
+
+def test_simplified_match_matrix_matches_reference(golden, tracer):
+    g = golden("match")
+    x, l1, l2, cand = _data.match_inputs(g)
+    s = SimplifiedHierarchicalRQ(HierarchicalRQKMeansConfig(**CFG), device=DEV)
+    seeded(72)
+    got = s._get_dynamic_match_matrix(torch.from_numpy(x).to(DEV), torch.from_numpy(l1).to(DEV),
+                                      torch.from_numpy(l2).to(DEV), torch.from_numpy(cand).to(DEV))
+    np_after, torch_after = np.random.randint(1 << 30, size=4), torch.randint(1 << 30, (4,)).numpy()
+    st = _certify.certify_trace(tracer.events)
+    owners = _certify.owners(tracer.events, "batched")
+    assert len(owners) == 1
+    fitted = [gi for gi, n in enumerate(SIZES) if n > NEED[2]]
+    diverged = _certify.diverged_segments(st, owners[0])
+    identical, excused, sync = _compare_builder(g, "simp", got.numpy().astype(np.uint8), fitted, diverged, np_after,
+                                                torch_after)
+    report("simp_match_matrix", identical_rows=identical, excused=excused, rng_in_sync=sync, fitted=len(fitted),
+           diverged_fits=sorted(diverged), **{k: v for k, v in st.items() if k != "segments"})
+
+
+def test_match_builders_sequential_and_lockstep_agree_on_golden_inputs(golden):
+    """Both GPU forms (lockstep sub-fits and the reference's one-after-another loop) on the golden inputs
+    give one matrix and one generator state (the lockstep form's RNG bookkeeping at this group mix)."""
+    g = golden("match")
+    x, l1, l2, cand = _data.match_inputs(g)
+    outs = []
+    for b in (True, False):
+        m = HierarchicalRQKMeans(HierarchicalRQKMeansConfig(**CFG), device=DEV)
+        m.batched_sub_fits = b
+        seeded(71)
+        mm = m._assign_last_match_matrix(torch.from_numpy(cand).to(DEV), 64, torch.from_numpy(x).to(DEV), NEED[0],
+                                         NEED[1], torch.from_numpy(l1), torch.from_numpy(l2), NEED[2], 16, 2)
+        outs.append((np.asarray(mm), np.random.randint(1 << 30, size=4)))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])

@@ -130,3 +130,85 @@ def test_sharded_semantic_id_trainer_writes_the_single_process_files(tmp_path):
         a = open(os.path.join(one, rel), "rb").read()
         b = open(os.path.join(two, rel), "rb").read()
         assert a == b, rel
+
+
+def _ckpt_worker(rank, world, port, x, seed, ck, np_state, t_state, resume, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _seeded(seed)
+        if np_state is not None:
+            np.random.set_state(np_state)
+            torch.set_rng_state(t_state)
+        m = HierarchicalRQKMeans(HierarchicalRQKMeansConfig(**CFG), checkpoint_dir=ck, device=DEV,
+                                 group=dist.group.WORLD)
+        res = m.train(x, resume=resume)
+        out.put((rank, np.stack([t.cpu().numpy() for t in res["cluster_ids"]], 1),
+                 [c.cpu().numpy() for c in m.cluster_centers_list], np.asarray(m.match_matrices[0])))
+    except Exception:
+        import traceback
+        out.put((rank, None, traceback.format_exc()))
+    dist.destroy_process_group()
+
+
+def test_resume_from_sharded_checkpoints_equals_uninterrupted_run(tmp_path, monkeypatch):
+    """a sharded run's checkpoints (rank 0 writes them, without residual data) resumed after the
+    last layer's checkpoint is lost -- by two ranks and by a single process, both rebuilding the residual
+    chain from ids and centres (_residual_chain) -- give the uninterrupted run's IDs, centres and match
+    matrix.  The generators are put where the uninterrupted run had them when its last layer started."""
+    import shutil
+    x = synth.small_mixture(2500, m=64, seed=21)
+    state = {}
+    orig = HierarchicalRQKMeans._train_last_layer
+
+    def recording(self, X, layer):
+        state["np"], state["torch"] = np.random.get_state(), torch.get_rng_state()
+        return orig(self, X, layer)
+    monkeypatch.setattr(HierarchicalRQKMeans, "_train_last_layer", recording)
+    _seeded(42)
+    ref = HierarchicalRQKMeans(HierarchicalRQKMeansConfig(**CFG), device=DEV)
+    rr = ref.train(x, resume=False)
+    monkeypatch.setattr(HierarchicalRQKMeans, "_train_last_layer", orig)
+    ids_ref = np.stack([t.cpu().numpy() for t in rr["cluster_ids"]], 1)
+    cents_ref = [c.cpu().numpy() for c in ref.cluster_centers_list]
+    match_ref = np.asarray(ref.match_matrices[0])
+
+    def same(ids, cents, match):
+        assert np.array_equal(ids, ids_ref)
+        for c, cr in zip(cents, cents_ref):
+            np.testing.assert_allclose(c, cr, rtol=1e-6, atol=1e-6)
+        assert np.array_equal(match, match_ref)
+
+    ck = str(tmp_path / "ck")
+    for r in _run(_ckpt_worker, 2, (x, 42, ck, None, None, False)):
+        same(*r[1:])
+    os.remove(os.path.join(ck, "layer_2_checkpoint.npz"))
+    ck2 = str(tmp_path / "ck2")
+    shutil.copytree(ck, ck2)
+    for r in _run(_ckpt_worker, 2, (x, 42, ck, state["np"], state["torch"], True)):
+        same(*r[1:])
+    np.random.set_state(state["np"])
+    torch.set_rng_state(state["torch"])
+    m = HierarchicalRQKMeans(HierarchicalRQKMeansConfig(**CFG), checkpoint_dir=ck2, device=DEV)
+    res = m.train(x, resume=True)
+    same(np.stack([t.cpu().numpy() for t in res["cluster_ids"]], 1), [c.cpu().numpy() for c in m.cluster_centers_list],
+         np.asarray(m.match_matrices[0]))
+
+
+def test_encoder_cache_follows_codebook_changes():
+    """the cached fused encoder is rebuilt when a codebook is replaced or edited in place."""
+    x = synth.small_mixture(2500, m=64, seed=21)
+    _seeded(42)
+    m = HierarchicalRQKMeans(HierarchicalRQKMeansConfig(**CFG), device=DEV)
+    m.train(x, resume=False)
+    a = m.predict(x[:300], reference_quirks=False)
+    c0 = m.cluster_centers_list[0]
+    c0[[0, 1]] = c0[[1, 0]].clone()  # in place: ids 0 and 1 of level 0 swap
+    b = m.predict(x[:300], reference_quirks=False)
+    assert np.array_equal(np.where(a[:, 0] == 0, 1, np.where(a[:, 0] == 1, 0, a[:, 0])), b[:, 0])
+    restored = c0.clone()
+    restored[[0, 1]] = c0[[1, 0]]
+    m.cluster_centers_list = [restored] + m.cluster_centers_list[1:]  # replaced by a new tensor: the original
+    assert np.array_equal(m.predict(x[:300], reference_quirks=False), a)

@@ -54,6 +54,38 @@ def test_auction_random_and_tied_match_oracle(n, k, levels):
         assert rounds == 1002  # the leftover rule ends it (Appendix A item 6)
 
 
+# the last layer's candidate-fit widths (hierarchical_rq_kmeans.py:792-801: K = 1280 PROD, 2560 XL), with
+# N % K == 0 and != 0 (1002 rounds, on the 2-byte-load path: N % 4 != 0) and heavily tied levels
+@pytest.mark.parametrize("n,k,levels", [(2560, 1280, 0), (2560, 1280, 5), (1501, 1280, 0), (5120, 2560, 0),
+                                        (5120, 2560, 7)])
+def test_auction_candidate_fit_widths_match_oracle(n, k, levels):
+    rng = np.random.default_rng(n * k + 7)
+    d = rng.random((n, k), dtype=np.float32) * 4
+    if levels:
+        d = np.round(d * levels) / levels
+    scores = (-d).astype(np.float16)
+    got, rounds = gpu_auction(scores)
+    ref = O.auction_lap_half(scores.astype(np.float32), tie_rule="stable")
+    assert (got == ref).all()
+    if n % k:
+        assert rounds == 1002
+
+
+def test_auction_half_scores_k1280_match_oracle():
+    """fp16 pairwise_distance_half scores (the candidate fits' input, :546-574 via balancekmeans.py) of
+    unit-norm rows: values crowd into few fp16 levels, so the topk boundary is full of equal values."""
+    x = synth.small_mixture(2560, m=200, seed=31)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    c = x[np.random.default_rng(3).choice(2560, 1280, replace=False)] + np.float32(0.01)
+    w = ops.auction_scores(torch.from_numpy(x.astype(np.float32)).to(DEV), torch.from_numpy(c.astype(np.float32)).to(DEV),
+                           half=True)
+    a, rounds = ops.auction(w)
+    s16 = w.cpu().numpy().T
+    ref = O.auction_lap_half(s16.astype(np.float32), tie_rule="stable")
+    assert (a.cpu().numpy().astype(np.int64) == ref).all()
+    assert len(np.unique(s16)) < s16.size // 100  # heavily tied
+
+
 @pytest.mark.parametrize("tag", ["n64k8", "n67k8", "n1000k16", "n5k8", "n96k8"])
 def test_auction_full_golden_inputs_match_reference(golden, tag):
     """fp32 auction (auction_lap_full, A6) on the reference's own outputs (tests/golden/auction_full.npz,

@@ -213,3 +213,80 @@ def test_csv_loader_matches_reference(golden, tmp_path, reader):
     ids_h, x_h = load(str(p), 4, [600])
     assert str(g["emb_half_dtype"]) == "torch.float16" and x_h.dtype == np.float16
     assert np.array_equal(x_h.view(np.uint16), g["emb_half"].view(np.uint16))
+
+
+# ----------------------------------------------------------------- match-matrix builders (§8f row 2)
+@pytest.mark.parametrize("variant", ["hier", "simp"])
+def test_match_builders_match_reference(golden, variant):
+    """The oracle's restatements of _assign_last_match_matrix (:968-1053) and _get_dynamic_match_matrix
+    (simplified…:247-303), replaying the reference's recorded sub-K-Means results, give the reference's
+    match matrix, the reference's greedy operands and leave both generators where the reference did."""
+    g = golden("match")
+    x, l1, l2, cand = _data.match_inputs(g)
+    need = _data.MATCH_NEED
+    sizes = _data.MATCH_SIZES
+    subs = []
+    if variant == "hier":
+        np.random.seed(71)
+        torch.manual_seed(71)
+        fits = [g["hier_fitted"][g["hier_fitted_off"][i]:g["hier_fitted_off"][i + 1]]
+                for i in range(len(g["hier_fitted_off"]) - 1)]
+        got = O.assign_last_match_matrix(x, l1, l2, cand, need[0], need[1], need[2], 2 * need[2],
+                                         O.recorded_fits(fits, need[2]), subs_out=subs)
+        want_sub, want_off = g["hier_sub"], g["hier_sub_off"]
+    else:
+        np.random.seed(72)
+        torch.manual_seed(72)
+        off = g["simp_sub_off"]
+        fits = [g["simp_sub"][off[gi]:off[gi + 1]] for gi, n in enumerate(sizes) if n > need[2]]
+        got = O.dynamic_match_matrix(x, l1, l2, cand, need[0], need[1], need[2],
+                                     O.recorded_fits(fits, need[2]), subs_out=subs)
+        want_sub, want_off = g["simp_sub"], g["simp_sub_off"]
+    np_after = np.random.randint(1 << 30, size=4)
+    torch_after = torch.randint(1 << 30, (4,)).numpy()
+    assert len(subs) == len(want_off) - 1
+    for i, s in enumerate(subs):
+        assert np.array_equal(s, want_sub[want_off[i]:want_off[i + 1]])
+    assert np.array_equal(got, g[f"{variant}_match"])
+    assert np.array_equal(np_after, g[f"{variant}_np_after"])
+    assert np.array_equal(torch_after, g[f"{variant}_torch_after"])
+    assert (got.sum(1)[np.asarray(sizes) > 0] == need[2]).all() if variant == "hier" else (got.sum(1) == need[2]).all()
+
+
+def test_greedy_certificate_on_reference_operands(golden):
+    """On the reference's own greedy operands the certificate's determined columns are in the reference's
+    row, and at an undetermined step (an fp32 near tie under the any-order bound, or the duplicated
+    candidate pair 5 / 63) the reference took one of the tied columns: the certificate the GPU parity
+    test relies on is consistent with the reference."""
+    g = golden("match")
+    x, l1, l2, cand = _data.match_inputs(g)
+    need = _data.MATCH_NEED[2]
+    off = g["hier_sub_off"]
+    rows = [gi for gi, n in enumerate(_data.MATCH_SIZES) if n > 0]
+    for k, gi in enumerate(rows):
+        sub = g["hier_sub"][off[k]:off[k + 1]]
+        cert = O.greedy_certificate(sub, cand, min(len(sub), need))
+        row = g["hier_match"][gi]
+        assert row[cert["taken"]].all()
+        if not cert["determined"]:
+            assert row[cert["tied"]].any(), cert
+
+
+@pytest.mark.parametrize("tag", sorted(_data.CONFIG0_CASES))
+def test_config0_single_level_matches_reference(golden, tag):
+    """BASELINE configs[0] (SimplifiedHierarchicalRQ with one level, simplified…:193-202): the oracle's
+    fit_by_min_loss with target_nodes_num = np.prod([]) = 1.0 and the reference's seeds reproduces the
+    reference's centres and per-song IDs (tests/golden/config0.npz).  The distances are the reference's
+    own torch.cdist call (O.torch_cdist_batched): with numpy's summation order instead, an fp16 score
+    rounds the other way somewhere in the K = 128 run and 12 of 128 centres part (a legitimate
+    order effect, certified on the GPU side by tests/_certify.py)."""
+    g = golden("config0")
+    x, k, it = _data.config0_inputs(tag, g)
+    target = np.prod([])
+    assert target == 1.0
+    torch.manual_seed(42)
+    rng = O.LegacyRNG(42, lambda n: torch.randint(n, (1,)).item())
+    c, _ = O.kmeans_fit(x, k, rng, iter_limit=it, balanced=True, min_loss_target=target,
+                        dist_fn=O.torch_cdist_batched)
+    np.testing.assert_allclose(c, g[f"{tag}_centers"], rtol=1e-5, atol=1e-5)
+    assert np.array_equal(O.torch_cdist_batched(x, c).argmin(1), g[f"{tag}_ids"][:, 0])

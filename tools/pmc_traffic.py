@@ -19,7 +19,7 @@ def short(n):
     return n.split("(")[0]
 
 
-def main(root):
+def main(root, rows):
     vals = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
         per = defaultdict(float)
@@ -41,8 +41,8 @@ def main(root):
         if fetch and write:
             out[k]["hbm_bytes"] = out[k]["fetch_bytes"] + out[k]["write_bytes"]
     print(json.dumps({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), FETCH_SIZE x2 (gfx950)",
-                      "kernels": out}, indent=1))
+                      "rows": rows, "kernels": out}, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)

@@ -16,4 +16,12 @@ for c in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "pass $c rc=$rc"
   [ $rc -ne 0 ] && { tail -5 "$OUT/p$i.log"; exit $rc; }
 done
-python3 "$GRAFT_REPO_ROOT/tools/pmc_traffic.py" "$OUT" > "$OUT/traffic.json" && cat "$OUT/traffic.json"
+# rows per launch of the profiled bench (bench.py compares it with its own --rows before using the bytes)
+ROWS=$(python3 - "$OUT/p1.log" <<'PY'
+import json, sys
+for l in open(sys.argv[1]):
+    if l.startswith("{"):
+        print(json.loads(l)["config"]["rows_per_gpu"])
+PY
+)
+python3 "$GRAFT_REPO_ROOT/tools/pmc_traffic.py" "$OUT" $ROWS > "$OUT/traffic.json" && cat "$OUT/traffic.json"
