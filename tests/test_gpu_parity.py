@@ -534,3 +534,38 @@ def test_rescore_two_rows_per_wave_equals_one(k, dim):
     assert (a == b).all()
     sel = np.arange(0, len(x), 7)
     assert (a[sel] == exact_ids(x[sel], c)).all()
+
+
+@pytest.mark.parametrize("k,dups", [(2560, 0), (1280, 0), (2560, 12)])
+def test_rescreen_of_overflowing_rows_keeps_exact_ids(k, dups, monkeypatch):
+    """The fp32 re-screen (assign.hip assign_rescreen_kernel, VERDICT r3 "re-score cliff"): diffuse unit
+    rows against K = 1280 / 2560 unit centres (the training-time nearest of residual codebooks) leave most
+    rows with more than 8 candidates inside the fp16 screen's bound.  With the re-screen those rows get an
+    fp32 list first; the IDs equal the all-candidate fp64 pass (RQSID_NO_RESCREEN=1) and the exact oracle,
+    also when 12 exact duplicates of one centre keep a true > 8-way tie overflowing (fp64 fallback, lowest
+    index).  Times both forms (printed)."""
+    import time
+    rng = np.random.default_rng(k + dups)
+    x = rng.standard_normal((30000, 512), dtype=np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    c = rng.standard_normal((k, 512), dtype=np.float32)
+    c /= np.linalg.norm(c, axis=1, keepdims=True)
+    if dups:
+        c[100:100 + dups] = c[7]
+        x[:500] = c[7] + np.float32(0.01) * rng.standard_normal((500, 512), dtype=np.float32)
+    pc = ops.prepare_centers(gpu(c))
+    xg = gpu(x)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("RQSID_NO_RESCREEN", mode)
+        ops.nearest(xg, pc)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        out[mode] = ops.nearest(xg, pc).cpu().numpy()
+        torch.cuda.synchronize()
+        print(f"k={k} dups={dups} rescreen={'off' if mode == '1' else 'on'}: {(time.perf_counter() - t) * 1e3:.2f} ms")
+    assert np.array_equal(out["0"], out["1"])
+    smp = np.arange(0, len(x), 7)
+    assert np.array_equal(out["0"][smp], exact_ids(x[smp], c))
+    if dups:
+        assert (out["0"][:500] == 7).all()
