@@ -95,7 +95,17 @@ struct SegAuction {
   uint32_t* s_sel;
   uint8_t* s_flag;
   int32_t* s_rounds;
+  // bid list (single auction, S = 1): the guessed pass appends every value whose key is at least
+  // last round's threshold key minus kListDelta (the window slots >= dlist and the values above the
+  // window) to its worker's list; when the round's threshold is a hit inside that range, the list holds
+  // every value that can bid and the bid pass walks the lists instead of sweeping W.  lflag != 0: some
+  // worker's threshold fell below its list base or its list overflowed: the sweep runs this round.
+  uint2* lst;                    // [K][lcap]: {job, value bits}
+  uint32_t* lcnt;                // [K][kAbovePad]: entries appended this round
+  uint32_t* lflag;               // [1]
+  int32_t lcap;
 };
+constexpr int kListDelta = 64;   // keys below last round's threshold kept in the bid list
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ off, int n_seg, int64_t i) {
   int lo = 0, hi = n_seg - 1;  // last s with off[s] <= i
@@ -451,6 +461,68 @@ __device__ __forceinline__ void guess_values(const ChunkScores& cs, const LaneJo
   }
 }
 
+// the list slot of each worker's values: d >= dlist (d as in guess_worker: the offset of the value's
+// key from the window base, 256 = above the window), i.e. keys >= T_prev - kListDelta
+__device__ __forceinline__ int32_t list_dmin(uint32_t T) {
+  if (T == 0) return 0x7FFFFFFF;  // no threshold yet (round 0: every worker takes the exact passes)
+  return max(0, (int32_t)(T & 0xFFFFu) - kListDelta - window_base(T));
+}
+
+// Append this block's values of the list range to their workers' lists: the window histogram gives each
+// worker's count (slots >= dlist and the above slot), one global atomic per (block, worker) reserves the
+// range, an LDS counter places each value inside it (order inside a block's range is arbitrary; the bid
+// pass ranks equal values by job index).  A worker whose list would overflow raises lflag.
+template <bool VEC>
+__device__ __forceinline__ void list_append(const SegAuction& a, const ChunkInfo& ci, const ChunkScores& cs,
+                                            const LaneJobs& lj, const _Float16 (&nc)[kJPT], const int32_t (&addk)[kKG],
+                                            uint32_t negbin, bool dead, int w0, int nw, uint32_t* h) {
+  __shared__ uint32_t lbase[kKG], lpos[kKG];
+  __shared__ int32_t ldm[kKG];
+  __syncthreads();  // the histogram flush above read h
+  // per worker: count of slots >= dlist (16 threads per worker, 16 slots each, + the above slot)
+  {
+    const int g = threadIdx.x >> 4, q = threadIdx.x & 15;
+    int32_t dm = 0;
+    uint32_t part = 0;
+    if (g < nw) {
+      dm = list_dmin(a.sel[((int64_t)ci.s * a.K + w0 + g) * 4 + 2]);
+      for (int sl = q * 16; sl < q * 16 + 16; ++sl) part += sl >= dm ? h[g * kGStride + sl] : 0u;
+      if (q == 0) part += h[g * kGStride + 256];
+    }
+    for (int o = 8; o > 0; o >>= 1) part += (uint32_t)__shfl_xor((int)part, o);
+    if (q == 0 && g < kKG) {
+      ldm[g] = dm;
+      lpos[g] = 0;
+      uint32_t b = 0;
+      if (g < nw && part) {
+        b = atomicAdd(&a.lcnt[(int64_t)(w0 + g) * kAbovePad], part);
+        if (b + part > (uint32_t)a.lcap) *a.lflag = 1;
+      }
+      lbase[g] = b;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < kKG; ++g) {
+    if (g >= nw) break;
+    const int w = w0 + g;
+    const int32_t addg = addk[g], dm = ldm[g];
+    const bool neg = (negbin >> g) & 1u;
+#pragma unroll
+    for (int t = 0; t < kJPT; ++t) {
+      const _Float16 x = __builtin_bit_cast(_Float16, cs.v[t][g]) + (lj.hb[t] == w ? (_Float16)0.0f : nc[t]);
+      const uint32_t b = __builtin_bit_cast(uint16_t, x);
+      int32_t d = neg ? addg - (int32_t)b : (int32_t)(int16_t)b + addg;
+      if (dead) d += lj.dead[t];
+      if (d >= dm) {
+        const uint32_t pos = lbase[g] + atomicAdd(&lpos[g], 1u);
+        if (pos < (uint32_t)a.lcap)
+          a.lst[(int64_t)w * a.lcap + pos] = make_uint2((uint32_t)(ci.j0 + job_of<VEC>(t)), b);
+      }
+    }
+  }
+}
+
 template <bool VEC>
 __global__ __launch_bounds__(256) void sa_guess_hist_kernel(SegAuction a) {
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
@@ -501,6 +573,7 @@ __global__ __launch_bounds__(256) void sa_guess_hist_kernel(SegAuction a) {
     const uint32_t c = h[(i >> 8) * kStride + (i & 255)];
     if (c) atomicAdd(&a.hist[(hw0 + (i >> 8)) * 256 + (i & 255)], c);
   }
+  if (a.lst) list_append<VEC>(a, ci, cs, lj, nc, addk, negbin, low && ci.nj < kCh, w0, nw, h);
 }
 
 // one wave per (segment, worker) of the multi-chunk segments
@@ -606,6 +679,8 @@ __global__ __launch_bounds__(256) void sa_select_guess_kernel(SegAuction a) {
   uint32_t b = 0, above = 0;
   if (hit) wave_select(h, rank - ab, b, above);
   if (lane == 0) {
+    // the bid list holds the keys >= T_prev - kListDelta: the new threshold must lie in that range
+    if (hit && a.lst && (int32_t)b < list_dmin(sel[2])) *a.lflag = 1;
     if (hit) {
       const uint32_t T = (uint32_t)window_base(sel[2]) + b;
       sel[0] = T >> 8;
@@ -899,6 +974,19 @@ __device__ __forceinline__ void resolve_chunk(const SegAuction& a, const ChunkIn
     k[t] = a.key[j];
     c[t] = a.cost[j];
   }
+  if (a.lst) {  // list mode: the retention / leftover bids of pairs no list held (the sweep's overrides)
+    const int counter = *a.round_dev;
+    const uint32_t ek = (uint32_t)a.eps[ci.s] << 16;
+    if (counter < 100 || counter > 1000) {
+#pragma unroll
+      for (int t = 0; t < kJPT; ++t) {
+        const int64_t j = ci.j0 + min((int64_t)(t * 256 + threadIdx.x), ci.nj - 1);
+        const int32_t hbj = a.hb[j];
+        if (counter < 100 && hbj >= 0) k[t] = max(k[t], ek | (0xFFFFu - (uint32_t)hbj));
+        if (counter > 1000 && a.nobid[j]) k[t] = max(k[t], ek | 0xFFFFu);
+      }
+    }
+  }
   uint32_t cnt = 0;
 #pragma unroll
   for (int t = 0; t < kJPT; ++t) {
@@ -1001,6 +1089,7 @@ __global__ __launch_bounds__(256) RQ_BID_ATTR void sa_bid_kernel(SegAuction a) {
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
   if (!(f & kLive)) return;
+  if (a.lst && !(f & kSingle) && !*a.any_miss && !*a.lflag) return;  // the list pass bids this round
   __shared__ uint4 eqc[kKG][4];  // per (worker, wave): values equal to T in each job slice
   __shared__ uint32_t gneed[kKG], goff[kKG];
   const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
@@ -1107,6 +1196,59 @@ __global__ __launch_bounds__(256) RQ_BID_ATTR void sa_bid_kernel(SegAuction a) {
     if (best[t] >> 16) atomicMax(&a.key[ci.j0 + job_of<VEC>(t)], best[t]);
 }
 
+// ---- the list pass (single auction): each worker's bids from its list, with the sweep's arithmetic ----
+// A value above T bids fp16(fp16(x - T) + eps); a value equal to T bids eps when it is among the first
+// `need` equal values in job order: all-or-none per chunk from the tie offsets (eqcnt / eqtot), and in the
+// one straddling chunk by its rank among the chunk's equal values (its list entries are one contiguous
+// range: one reservation per (chunk, worker)).  The retention (round < 100: the previous winner bids eps)
+// and leftover (round > 1000: worker 0 bids eps on jobs without a bidder) overrides apply to listed pairs
+// here; resolve adds them for pairs outside the lists.
+__global__ __launch_bounds__(256) void sa_list_bid_kernel(SegAuction a) {
+  if (!(a.flag[0] & kLive) || *a.any_miss || *a.lflag) return;
+  const int w = blockIdx.y;
+  const uint32_t n = min(a.lcnt[(int64_t)w * kAbovePad], (uint32_t)a.lcap);
+  const int counter = *a.round_dev;
+  const uint16_t eps = a.eps[0];
+  const _Float16 epsh = __builtin_bit_cast(_Float16, eps);
+  const uint32_t kT = a.sel[(int64_t)w * 4 + 2], need = a.sel[(int64_t)w * 4 + 3];
+  const _Float16 vT = __builtin_bit_cast(_Float16, okey_inv(kT));
+  const uint32_t* e = a.eqcnt + (int64_t)w * a.total_chunks;
+  const uint32_t etot = a.eqtot[w];
+  const int64_t c_last = a.chunk_off[1] - 1;
+  const uint2* L = a.lst + (int64_t)w * a.lcap;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const uint2 en = L[i];
+    const uint32_t j = en.x;
+    const _Float16 x = __builtin_bit_cast(_Float16, (uint16_t)en.y);
+    uint32_t bid = 0;
+    if (x > vT) {
+      bid = __builtin_bit_cast(uint16_t, (_Float16)((_Float16)(x - vT) + epsh));
+    } else if (x == vT) {
+      const int64_t c = j / kCh;
+      const uint32_t off = e[c], nc = (c < c_last ? e[c + 1] : etot) - off;
+      if (need >= off + nc) {
+        bid = eps;
+      } else if (need > off) {
+        uint32_t rank = 0;  // equal values of this chunk with a smaller job (the chunk's range around i)
+        for (uint32_t k = i; k-- > 0;) {
+          const uint2 o = L[k];
+          if (o.x / kCh != (uint32_t)c) break;
+          rank += __builtin_bit_cast(_Float16, (uint16_t)o.y) == vT && o.x < j;
+        }
+        for (uint32_t k = i + 1; k < n; ++k) {
+          const uint2 o = L[k];
+          if (o.x / kCh != (uint32_t)c) break;
+          rank += __builtin_bit_cast(_Float16, (uint16_t)o.y) == vT && o.x < j;
+        }
+        if (off + rank < need) bid = eps;
+      }
+    }
+    if (counter < 100 && a.hb[j] == w) bid = eps;
+    if (counter > 1000 && w == 0 && a.nobid[j]) bid = eps;
+    if (bid) atomicMax(&a.key[j], (bid << 16) | (0xFFFFu - (uint32_t)w));
+  }
+}
+
 // ---- resolve: per job of the live segments, one block per chunk ----
 __global__ __launch_bounds__(256) void sa_resolve_kernel(SegAuction a, int32_t* __restrict__ out) {
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
@@ -1123,7 +1265,10 @@ __global__ __launch_bounds__(256) void sa_round_end_kernel(SegAuction a, int cou
     *a.round_dev += 1;
     if (a.any_miss) *a.any_miss = 0;  // for the next round's select_guess (a store at the top of the guessed
                                       // pass would turn its uniform loads into vector loads)
+    if (a.lflag) *a.lflag = 0;
   }
+  if (a.lst && blockIdx.x == 0)
+    for (int w = threadIdx.x; w < a.K; w += 256) a.lcnt[(int64_t)w * kAbovePad] = 0;
   uint32_t live = 0;
   if (s < a.S && (a.flag[s] & kLive)) {
     const int64_t n_s = a.n_glob ? a.n_glob : a.seg_off[s + 1] - a.seg_off[s];
@@ -1246,6 +1391,13 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.s_sel = snap ? c.take<uint32_t>((int64_t)S * K * 4 + 1) : nullptr;  // + the round number
   a.s_flag = snap ? c.take<uint8_t>(S) : nullptr;
   a.s_rounds = snap ? c.take<int32_t>(S) : nullptr;
+  // the bid lists: one single auction of several chunks (RQSID_AUCTION_LIST=0: the sweep, for A/B)
+  const char* el = getenv("RQSID_AUCTION_LIST");
+  const bool list = guess && S == 1 && a.n_multi == 1 && !(el && !atoi(el));
+  a.lcap = list ? (int32_t)std::min<int64_t>(4 * (N / K) + 1024, INT32_MAX / 2) : 0;
+  a.lst = list ? c.take<uint2>((int64_t)K * a.lcap) : nullptr;
+  a.lcnt = list ? c.take<uint32_t>((int64_t)K * kAbovePad) : nullptr;
+  a.lflag = list ? c.take<uint32_t>(1) : nullptr;
 }
 
 }  // namespace
@@ -1355,6 +1507,10 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   // lean rounds leave out the two-pass kernels of missed workers (five launches of a few us each, empty
   // in most rounds); a lean block runs from a snapshot of the round state and is replayed with the full
   // rounds when any worker missed in it, so the result is the full rounds' in every case
+  const unsigned lgx = a.lst ? (unsigned)std::min<int64_t>(cdiv(a.lcap / 2, 256), 16) : 1;
+  if (a.lst && (hipMemsetAsync(a.lcnt, 0, (size_t)n_workers * kAbovePad * 4, st) != hipSuccess ||
+                hipMemsetAsync(a.lflag, 0, 4, st) != hipSuccess))
+    return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   auto launch_round = [&](hipStream_t q, bool count, bool lean) {
     if (n_multi > 0) {
       if (vec) hipLaunchKernelGGL((sa_guess_hist_kernel<true>), gcw, dim3(256), 0, q, a);
@@ -1377,6 +1533,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     if (any_single) hipLaunchKernelGGL(sa_small_select_kernel, gcw, dim3(256), 0, q, a);
     if (vec) hipLaunchKernelGGL((sa_bid_kernel<true>), gcw, dim3(256), 0, q, a);
     else hipLaunchKernelGGL((sa_bid_kernel<false>), gcw, dim3(256), 0, q, a);
+    if (a.lst) hipLaunchKernelGGL(sa_list_bid_kernel, dim3(lgx, (unsigned)a.K), dim3(256), 0, q, a);
     hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, q, a, out_assign);
     hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
   };

@@ -356,3 +356,31 @@ def test_sharded_balanced_fit_world1(tmp_path):
         torch.testing.assert_close(sl.cluster_centers, km.cluster_centers, rtol=1e-6, atol=1e-6)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,k,half", [(200_000, 128, False), (100_000, 1280, True), (60_001, 1280, True)])
+def test_auction_bid_list_equals_sweep(n, k, half, monkeypatch):
+    """The bid-list pass of the single auction (auction_seg.hip sa_list_bid_kernel: each worker bids from the
+    values the guessed pass listed, keys >= last threshold - 64) gives the sweep's assignment and round count
+    (RQSID_AUCTION_LIST=0) on the level-0 (K = 128) and candidate-fit (K = 1280, fp16 cdist) shapes, with the
+    retention (round < 100) and leftover (round > 1000, N % K != 0) rules; times both (printed)."""
+    import time
+    x = synth.small_mixture(n, m=3000, seed=k)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    xg = torch.from_numpy(x.astype(np.float32)).to(DEV)
+    c = xg[torch.from_numpy(np.random.default_rng(k).choice(n, k, replace=False)).to(DEV)] * 0.9
+    w = ops.auction_scores(xg, c, half=half)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("RQSID_AUCTION_LIST", mode)
+        ops.auction(w)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        a, rounds = ops.auction(w)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        out[mode] = (a.cpu().numpy(), rounds)
+        print(f"n={n} k={k} list={mode}: {rounds} rounds, {dt * 1e3 / rounds:.3f} ms/round")
+    assert np.array_equal(out["1"][0], out["0"][0]) and out["1"][1] == out["0"][1]
+    if n % k:
+        assert out["1"][1] == 1002

@@ -45,13 +45,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--out", default="")
+    ap.add_argument("--preset", choices=("prod", "xl"), default="prod",
+                    help="prod: need [128,128,256], lc [128,1280,1280]; xl (configs[4]): need [256,256,512], "
+                         "lc [256,2560,2560] (run at its per-rank share, 6.25M rows)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     n = a.rows
-    need, lc = [128, 128, 256], [128, 1280, 1280]
+    need, lc = ([128, 128, 256], [128, 1280, 1280]) if a.preset == "prod" else ([256, 256, 512], [256, 2560, 2560])
     x = bench.make_rows(n, 0, dev)
     g = torch.Generator(device=dev).manual_seed(7)
-    res = {"rows": n, "phases": {}}
+    res = {"rows": n, "preset": a.preset, "need_clusters": need, "layer_clusters": lc, "phases": {}}
 
     # level 0: K=128 balanced fit_by_min_loss iteration
     c0 = x[torch.randperm(n, device=dev, generator=g)[:need[0]]].clone()
@@ -91,7 +94,7 @@ def main():
                                "parents": int((sizes > 0).sum()), "projected_s": round(t1 * it1, 1)}
     del xo
 
-    # candidate fits: K=1280 with fp16 distances (half: K >= 512), 20 iterations, two fits
+    # candidate fits: K=lc[2] (1280 / 2560) with fp16 distances (half: K >= 512), 20 iterations, two fits
     cc = x[torch.randperm(n, device=dev, generator=g)[:lc[2]]].clone()
 
     def candidates():
@@ -104,7 +107,7 @@ def main():
     res["phases"]["candidates"] = {"s_per_iteration": round(t2, 3), "auction_rounds": r2, "iterations": 2 * 20,
                                    "projected_s": round(t2 * 40, 1)}
 
-    # match-matrix groups: (l1, l2) groups of >= 2 need rows fit K=256 (iterations of the group size)
+    # match-matrix groups: (l1, l2) groups of >= 2 need rows fit K=need[2] (iterations of the group size)
     groups = need[0] * need[1]
     gid = torch.randint(0, groups, (n,), device=dev, generator=g)
     gs = torch.bincount(gid, minlength=groups).cpu().numpy()
@@ -113,6 +116,7 @@ def main():
         keep = torch.isin(gid, torch.from_numpy(big).to(dev))
         rows = torch.nonzero(keep).flatten()
         order = rows[torch.sort(gid[rows], stable=True)[1]]
+        del rows, keep
         xg = x[order].contiguous()
         bs = gs[big]
         layg = ops.SegmentLayout(bs, dev)
@@ -131,6 +135,10 @@ def main():
         res["phases"]["groups"] = {"s_per_iteration": round(t3, 3), "auction_rounds_max": r3, "iterations": it3,
                                    "groups": int(len(big)), "rows": int(bs.sum()), "projected_s": round(t3 * it3, 1),
                                    "note": "uniform random (l1,l2) groups: a trained model's groups are uneven"}
+    else:
+        res["phases"]["groups"] = {"groups": 0, "projected_s": 0.0,
+                                   "note": f"no (l1,l2) group of a uniform random split reaches {2 * need[2]} rows: "
+                                           "every group takes its rows / a row sample (no sub-fit)"}
     res["projected_total_s"] = round(sum(p["projected_s"] for p in res["phases"].values()), 1)
     res["method"] = ("one timed iteration per phase after a warm-up, x the reference's iteration schedule; "
                      "encode passes and host bookkeeping excluded")
