@@ -95,15 +95,16 @@ struct SegAuction {
   uint32_t* s_sel;
   uint8_t* s_flag;
   int32_t* s_rounds;
-  // bid list (single auction, S = 1): the guessed pass appends every value whose key is at least
-  // last round's threshold key minus kListDelta (the window slots >= dlist and the values above the
-  // window) to its worker's list; when the round's threshold is a hit inside that range, the list holds
-  // every value that can bid and the bid pass walks the lists instead of sweeping W.  lflag != 0: some
-  // worker's threshold fell below its list base or its list overflowed: the sweep runs this round.
-  uint2* lst;                    // [K][lcap]: {job, value bits}
-  uint32_t* lcnt;                // [K][kAbovePad]: entries appended this round
-  uint32_t* lflag;               // [1]
-  int32_t lcap;
+  // bid lists (multi-chunk segments): the guessed pass appends every value whose key is at least last
+  // round's threshold key minus kListDelta (the window slots >= dlist and the values above the window) to
+  // its (segment, worker) list; when the round's threshold is a hit inside that range, the list holds
+  // every value that can bid and the list pass bids from it.  lbad[hw] = 1: the worker missed, its
+  // threshold fell below its list base or its list overflowed; the sweep bids for its block this round.
+  uint2* lst;                    // per multi-chunk segment r: [K][lcs[r]] entries {job, value bits} at loff[r]
+  uint32_t* lcnt;                // [n_multi*K][kAbovePad]: entries appended this round
+  uint8_t* lbad;                 // [n_multi*K]
+  int64_t* loff;                 // [n_multi]
+  int32_t* lcs;                  // [n_multi]: capacity per worker, 4 * (N_s / K) + 256
 };
 constexpr int kListDelta = 64;   // keys below last round's threshold kept in the bid list
 
@@ -471,11 +472,12 @@ __device__ __forceinline__ int32_t list_dmin(uint32_t T) {
 // Append this block's values of the list range to their workers' lists: the window histogram gives each
 // worker's count (slots >= dlist and the above slot), one global atomic per (block, worker) reserves the
 // range, an LDS counter places each value inside it (order inside a block's range is arbitrary; the bid
-// pass ranks equal values by job index).  A worker whose list would overflow raises lflag.
+// pass ranks equal values by job index).  Entries past a worker's capacity are dropped (select_guess then
+// marks the worker for the sweep).
 template <bool VEC>
 __device__ __forceinline__ void list_append(const SegAuction& a, const ChunkInfo& ci, const ChunkScores& cs,
                                             const LaneJobs& lj, const _Float16 (&nc)[kJPT], const int32_t (&addk)[kKG],
-                                            uint32_t negbin, bool dead, int w0, int nw, uint32_t* h) {
+                                            uint32_t negbin, bool dead, int w0, int nw, int64_t hw0, uint32_t* h) {
   __shared__ uint32_t lbase[kKG], lpos[kKG];
   __shared__ int32_t ldm[kKG];
   __syncthreads();  // the histogram flush above read h
@@ -493,15 +495,13 @@ __device__ __forceinline__ void list_append(const SegAuction& a, const ChunkInfo
     if (q == 0 && g < kKG) {
       ldm[g] = dm;
       lpos[g] = 0;
-      uint32_t b = 0;
-      if (g < nw && part) {
-        b = atomicAdd(&a.lcnt[(int64_t)(w0 + g) * kAbovePad], part);
-        if (b + part > (uint32_t)a.lcap) *a.lflag = 1;
-      }
-      lbase[g] = b;
+      lbase[g] = g < nw && part ? atomicAdd(&a.lcnt[(hw0 + g) * kAbovePad], part) : 0u;
     }
   }
   __syncthreads();
+  const int r = a.hidx[ci.s];
+  const uint32_t cap = (uint32_t)a.lcs[r];
+  uint2* const L0 = a.lst + a.loff[r];
 #pragma unroll
   for (int g = 0; g < kKG; ++g) {
     if (g >= nw) break;
@@ -516,8 +516,7 @@ __device__ __forceinline__ void list_append(const SegAuction& a, const ChunkInfo
       if (dead) d += lj.dead[t];
       if (d >= dm) {
         const uint32_t pos = lbase[g] + atomicAdd(&lpos[g], 1u);
-        if (pos < (uint32_t)a.lcap)
-          a.lst[(int64_t)w * a.lcap + pos] = make_uint2((uint32_t)(ci.j0 + job_of<VEC>(t)), b);
+        if (pos < cap) L0[(int64_t)w * cap + pos] = make_uint2((uint32_t)(ci.j0 + job_of<VEC>(t)), b);
       }
     }
   }
@@ -573,7 +572,7 @@ __global__ __launch_bounds__(256) void sa_guess_hist_kernel(SegAuction a) {
     const uint32_t c = h[(i >> 8) * kStride + (i & 255)];
     if (c) atomicAdd(&a.hist[(hw0 + (i >> 8)) * 256 + (i & 255)], c);
   }
-  if (a.lst) list_append<VEC>(a, ci, cs, lj, nc, addk, negbin, low && ci.nj < kCh, w0, nw, h);
+  if (a.lst) list_append<VEC>(a, ci, cs, lj, nc, addk, negbin, low && ci.nj < kCh, w0, nw, hw0, h);
 }
 
 // one wave per (segment, worker) of the multi-chunk segments
@@ -680,7 +679,9 @@ __global__ __launch_bounds__(256) void sa_select_guess_kernel(SegAuction a) {
   if (hit) wave_select(h, rank - ab, b, above);
   if (lane == 0) {
     // the bid list holds the keys >= T_prev - kListDelta: the new threshold must lie in that range
-    if (hit && a.lst && (int32_t)b < list_dmin(sel[2])) *a.lflag = 1;
+    if (a.lst)
+      a.lbad[hw] = !hit || (int32_t)b < list_dmin(sel[2]) ||
+                   a.lcnt[hw * kAbovePad] > (uint32_t)a.lcs[hw / a.K];
     if (hit) {
       const uint32_t T = (uint32_t)window_base(sel[2]) + b;
       sel[0] = T >> 8;
@@ -1089,7 +1090,13 @@ __global__ __launch_bounds__(256) RQ_BID_ATTR void sa_bid_kernel(SegAuction a) {
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
   if (!(f & kLive)) return;
-  if (a.lst && !(f & kSingle) && !*a.any_miss && !*a.lflag) return;  // the list pass bids this round
+  if (a.lst && !(f & kSingle)) {  // the list pass bids for workers whose lists hold every bidding value
+    const int64_t hwb = (int64_t)a.hidx[ci.s] * a.K + blockIdx.y * kKG;
+    const int nwb = min(kKG, a.K - (int)blockIdx.y * kKG);
+    bool bad = false;
+    for (int g = 0; g < nwb; ++g) bad |= a.lbad[hwb + g] != 0;
+    if (!bad) return;  // (a block with one bad worker bids for all 16: the listed ones' keys are equal)
+  }
   __shared__ uint4 eqc[kKG][4];  // per (worker, wave): values equal to T in each job slice
   __shared__ uint32_t gneed[kKG], goff[kKG];
   const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
@@ -1204,18 +1211,22 @@ __global__ __launch_bounds__(256) RQ_BID_ATTR void sa_bid_kernel(SegAuction a) {
 // and leftover (round > 1000: worker 0 bids eps on jobs without a bidder) overrides apply to listed pairs
 // here; resolve adds them for pairs outside the lists.
 __global__ __launch_bounds__(256) void sa_list_bid_kernel(SegAuction a) {
-  if (!(a.flag[0] & kLive) || *a.any_miss || *a.lflag) return;
-  const int w = blockIdx.y;
-  const uint32_t n = min(a.lcnt[(int64_t)w * kAbovePad], (uint32_t)a.lcap);
+  const int64_t hw = blockIdx.y;
+  const int r = (int)(hw / a.K), w = (int)(hw % a.K);
+  const int sg = a.mseg[r];
+  if (!(a.flag[sg] & kLive) || a.lbad[hw]) return;
+  const uint32_t cap = (uint32_t)a.lcs[r];
+  const uint32_t n = min(a.lcnt[hw * kAbovePad], cap);
   const int counter = *a.round_dev;
-  const uint16_t eps = a.eps[0];
+  const uint16_t eps = a.eps[sg];
   const _Float16 epsh = __builtin_bit_cast(_Float16, eps);
-  const uint32_t kT = a.sel[(int64_t)w * 4 + 2], need = a.sel[(int64_t)w * 4 + 3];
+  const int64_t sw = (int64_t)sg * a.K + w;
+  const uint32_t kT = a.sel[sw * 4 + 2], need = a.sel[sw * 4 + 3];
   const _Float16 vT = __builtin_bit_cast(_Float16, okey_inv(kT));
   const uint32_t* e = a.eqcnt + (int64_t)w * a.total_chunks;
-  const uint32_t etot = a.eqtot[w];
-  const int64_t c_last = a.chunk_off[1] - 1;
-  const uint2* L = a.lst + (int64_t)w * a.lcap;
+  const uint32_t etot = a.eqtot[sw];
+  const int64_t j0 = a.seg_off[sg], c0 = a.chunk_off[sg], c_last = a.chunk_off[sg + 1] - 1;
+  const uint2* L = a.lst + a.loff[r] + (int64_t)w * cap;
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const uint2 en = L[i];
     const uint32_t j = en.x;
@@ -1224,7 +1235,7 @@ __global__ __launch_bounds__(256) void sa_list_bid_kernel(SegAuction a) {
     if (x > vT) {
       bid = __builtin_bit_cast(uint16_t, (_Float16)((_Float16)(x - vT) + epsh));
     } else if (x == vT) {
-      const int64_t c = j / kCh;
+      const int64_t cl = ((int64_t)j - j0) / kCh, c = c0 + cl;
       const uint32_t off = e[c], nc = (c < c_last ? e[c + 1] : etot) - off;
       if (need >= off + nc) {
         bid = eps;
@@ -1232,12 +1243,12 @@ __global__ __launch_bounds__(256) void sa_list_bid_kernel(SegAuction a) {
         uint32_t rank = 0;  // equal values of this chunk with a smaller job (the chunk's range around i)
         for (uint32_t k = i; k-- > 0;) {
           const uint2 o = L[k];
-          if (o.x / kCh != (uint32_t)c) break;
+          if (((int64_t)o.x - j0) / kCh != cl) break;
           rank += __builtin_bit_cast(_Float16, (uint16_t)o.y) == vT && o.x < j;
         }
         for (uint32_t k = i + 1; k < n; ++k) {
           const uint2 o = L[k];
-          if (o.x / kCh != (uint32_t)c) break;
+          if (((int64_t)o.x - j0) / kCh != cl) break;
           rank += __builtin_bit_cast(_Float16, (uint16_t)o.y) == vT && o.x < j;
         }
         if (off + rank < need) bid = eps;
@@ -1246,6 +1257,18 @@ __global__ __launch_bounds__(256) void sa_list_bid_kernel(SegAuction a) {
     if (counter < 100 && a.hb[j] == w) bid = eps;
     if (counter > 1000 && w == 0 && a.nobid[j]) bid = eps;
     if (bid) atomicMax(&a.key[j], (bid << 16) | (0xFFFFu - (uint32_t)w));
+  }
+}
+
+// list regions: segment r's K lists of 4 * (N_s / K) + 256 entries each, in multi-chunk segment order
+__global__ void sa_list_layout_kernel(SegAuction a) {
+  int64_t off = 0;
+  for (int r = 0; r < a.n_multi; ++r) {
+    const int s = a.mseg[r];
+    const int64_t cap = 4 * ((int64_t)(a.seg_off[s + 1] - a.seg_off[s]) / a.K) + 256;
+    a.loff[r] = off;
+    a.lcs[r] = (int32_t)cap;
+    off += cap * a.K;
   }
 }
 
@@ -1265,10 +1288,9 @@ __global__ __launch_bounds__(256) void sa_round_end_kernel(SegAuction a, int cou
     *a.round_dev += 1;
     if (a.any_miss) *a.any_miss = 0;  // for the next round's select_guess (a store at the top of the guessed
                                       // pass would turn its uniform loads into vector loads)
-    if (a.lflag) *a.lflag = 0;
   }
-  if (a.lst && blockIdx.x == 0)
-    for (int w = threadIdx.x; w < a.K; w += 256) a.lcnt[(int64_t)w * kAbovePad] = 0;
+  if (a.lst)
+    for (int64_t hw = s; hw < (int64_t)a.n_multi * a.K; hw += (int64_t)gridDim.x * 256) a.lcnt[hw * kAbovePad] = 0;
   uint32_t live = 0;
   if (s < a.S && (a.flag[s] & kLive)) {
     const int64_t n_s = a.n_glob ? a.n_glob : a.seg_off[s + 1] - a.seg_off[s];
@@ -1391,13 +1413,16 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.s_sel = snap ? c.take<uint32_t>((int64_t)S * K * 4 + 1) : nullptr;  // + the round number
   a.s_flag = snap ? c.take<uint8_t>(S) : nullptr;
   a.s_rounds = snap ? c.take<int32_t>(S) : nullptr;
-  // the bid lists: one single auction of several chunks (RQSID_AUCTION_LIST=0: the sweep, for A/B)
+  // the bid lists of the multi-chunk segments (RQSID_AUCTION_LIST=0: the sweep, for A/B): segment s holds
+  // K * (4 * (N_s / K) + 256) <= 4 N_s + 256 K entries
   const char* el = getenv("RQSID_AUCTION_LIST");
-  const bool list = guess && S == 1 && a.n_multi == 1 && !(el && !atoi(el));
-  a.lcap = list ? (int32_t)std::min<int64_t>(4 * (N / K) + 1024, INT32_MAX / 2) : 0;
-  a.lst = list ? c.take<uint2>((int64_t)K * a.lcap) : nullptr;
-  a.lcnt = list ? c.take<uint32_t>((int64_t)K * kAbovePad) : nullptr;
-  a.lflag = list ? c.take<uint32_t>(1) : nullptr;
+  const bool list = guess && a.n_multi > 0 && (int64_t)a.n_multi * K <= 65535 && !(el && !atoi(el));
+  const int64_t nm = a.n_multi > 0 ? a.n_multi : 1;
+  a.lst = list ? c.take<uint2>(4 * N + 256 * (int64_t)K * nm) : nullptr;
+  a.lcnt = list ? c.take<uint32_t>(nm * K * kAbovePad) : nullptr;
+  a.lbad = list ? c.take<uint8_t>(nm * K) : nullptr;
+  a.loff = list ? c.take<int64_t>(nm) : nullptr;
+  a.lcs = list ? c.take<int32_t>(nm) : nullptr;
 }
 
 }  // namespace
@@ -1507,10 +1532,14 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   // lean rounds leave out the two-pass kernels of missed workers (five launches of a few us each, empty
   // in most rounds); a lean block runs from a snapshot of the round state and is replayed with the full
   // rounds when any worker missed in it, so the result is the full rounds' in every case
-  const unsigned lgx = a.lst ? (unsigned)std::min<int64_t>(cdiv(a.lcap / 2, 256), 16) : 1;
-  if (a.lst && (hipMemsetAsync(a.lcnt, 0, (size_t)n_workers * kAbovePad * 4, st) != hipSuccess ||
-                hipMemsetAsync(a.lflag, 0, 4, st) != hipSuccess))
-    return fail(RQSID_E_LAUNCH, "seg_auction: memset");
+  // list pass grid: blocks per (segment, worker) for about twice the average list (~1.5 jobs per worker)
+  const unsigned lgx = (unsigned)std::min<int64_t>(std::max<int64_t>(cdiv(2 * n_jobs / std::max(1, n_multi) / n_workers, 256), 1), 16);
+  if (a.lst) {
+    if (hipMemsetAsync(a.lcnt, 0, (size_t)n_multi * n_workers * kAbovePad * 4, st) != hipSuccess ||
+        hipMemsetAsync(a.lbad, 1, (size_t)n_multi * n_workers, st) != hipSuccess)
+      return fail(RQSID_E_LAUNCH, "seg_auction: memset");
+    hipLaunchKernelGGL(sa_list_layout_kernel, dim3(1), dim3(1), 0, st, a);
+  }
   auto launch_round = [&](hipStream_t q, bool count, bool lean) {
     if (n_multi > 0) {
       if (vec) hipLaunchKernelGGL((sa_guess_hist_kernel<true>), gcw, dim3(256), 0, q, a);
@@ -1533,7 +1562,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     if (any_single) hipLaunchKernelGGL(sa_small_select_kernel, gcw, dim3(256), 0, q, a);
     if (vec) hipLaunchKernelGGL((sa_bid_kernel<true>), gcw, dim3(256), 0, q, a);
     else hipLaunchKernelGGL((sa_bid_kernel<false>), gcw, dim3(256), 0, q, a);
-    if (a.lst) hipLaunchKernelGGL(sa_list_bid_kernel, dim3(lgx, (unsigned)a.K), dim3(256), 0, q, a);
+    if (a.lst) hipLaunchKernelGGL(sa_list_bid_kernel, dim3(lgx, (unsigned)(n_multi * a.K)), dim3(256), 0, q, a);
     hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, q, a, out_assign);
     hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
   };

@@ -384,3 +384,27 @@ def test_auction_bid_list_equals_sweep(n, k, half, monkeypatch):
     assert np.array_equal(out["1"][0], out["0"][0]) and out["1"][1] == out["0"][1]
     if n % k:
         assert out["1"][1] == 1002
+
+
+def test_group_fits_k512_certified():
+    """configs[4]'s match-matrix group fits (hierarchical_rq_kmeans.py:1011-1018 with need[2] = 512: groups of
+    >= 1024 rows fit KMeans(512, balanced).fit, half=False) through the lockstep path (fit_segments), every
+    iteration of both segments certified against the oracle (tests/_certify.py)."""
+    from generative_ranking_recommender_amd import balancekmeans as bk
+    from tests import _certify
+    x = synth.small_mixture(2560, m=300, seed=77)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    sizes = [1024, 1536]
+    seeded(5)
+    inits = [[bk.init_indices(n, 512)] for n in sizes]
+    rec = _certify.Recorder()
+    bk.TRACE = rec
+    try:
+        c, a = bk.fit_segments(torch.from_numpy(x.astype(np.float32)).to(DEV), sizes, 512, [3, 3], inits, half=False)
+    finally:
+        bk.TRACE = None
+    st = _certify.certify_trace(rec.events)
+    assert st["auctions"] == st["steps"] and 2 <= st["steps"] <= 6
+    a = a.cpu().numpy()
+    for s0, s1 in ((0, 1024), (1024, 2560)):
+        assert np.bincount(a[s0:s1], minlength=512).max() == (s1 - s0) // 512  # N % K == 0: exactly balanced
