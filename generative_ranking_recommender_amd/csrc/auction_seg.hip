@@ -489,7 +489,7 @@ __device__ __forceinline__ void list_append(const SegAuction& a, const ChunkInfo
     if (g < nw) {
       dm = list_dmin(a.sel[((int64_t)ci.s * a.K + w0 + g) * 4 + 2]);
       for (int sl = q * 16; sl < q * 16 + 16; ++sl) part += sl >= dm ? h[g * kGStride + sl] : 0u;
-      if (q == 0) part += h[g * kGStride + 256];
+      if (q == 0 && dm <= 256) part += h[g * kGStride + 256];  // (no threshold yet: nothing listed)
     }
     for (int o = 8; o > 0; o >>= 1) part += (uint32_t)__shfl_xor((int)part, o);
     if (q == 0 && g < kKG) {
