@@ -95,14 +95,12 @@ struct SegAuction {
   uint32_t* s_sel;
   uint8_t* s_flag;
   int32_t* s_rounds;
-  // bid lists (multi-chunk segments): the guessed pass appends every value whose key is at least last
-  // round's threshold key minus kListDelta (the window slots >= dlist and the values above the window) to
-  // its (segment, worker) list; when the round's threshold is a hit inside that range, the list holds
-  // every value that can bid and the list pass bids from it.  lbad[hw] = 1: the worker missed, its
-  // threshold fell below its list base or its list overflowed; the sweep bids for its block this round.
-  uint2* lst;                    // per multi-chunk segment r: [K][lcs[r]] entries {job, value bits} at loff[r]
-  uint32_t* lcnt;                // [n_multi*K][kAbovePad]: entries appended this round
-  uint8_t* lbad;                 // [n_multi*K]
+  // bid lists (multi-chunk segments; sa_list_round_kernel explains them): per (segment, worker) the jobs
+  // whose value key was >= lkb when the list was built, with their raw scores
+  uint2* lst;                    // per multi-chunk segment r: [K][lcs[r]] entries {job, raw score bits} at loff[r]
+  uint32_t* lcnt;                // [n_multi*K][kAbovePad]: entries of the worker's list (0: no list)
+  uint32_t* lkb;                 // [n_multi*K]: the list's base key
+  uint8_t* lbad;                 // [n_multi*K]: 1 = the worker takes the sweep path this round
   int64_t* loff;                 // [n_multi]
   int32_t* lcs;                  // [n_multi]: capacity per worker, 4 * (N_s / K) + 256
 };
@@ -496,6 +494,8 @@ __device__ __forceinline__ void list_append(const SegAuction& a, const ChunkInfo
       ldm[g] = dm;
       lpos[g] = 0;
       lbase[g] = g < nw && part ? atomicAdd(&a.lcnt[(hw0 + g) * kAbovePad], part) : 0u;
+      if (g < nw && dm <= 256 && a.lbad[hw0 + g] && blockIdx.x == a.chunk_off[ci.s])  // (one block per worker)
+        a.lkb[hw0 + g] = (uint32_t)(window_base(a.sel[((int64_t)ci.s * a.K + w0 + g) * 4 + 2]) + dm);
     }
   }
   __syncthreads();
@@ -516,7 +516,7 @@ __device__ __forceinline__ void list_append(const SegAuction& a, const ChunkInfo
       if (dead) d += lj.dead[t];
       if (d >= dm) {
         const uint32_t pos = lbase[g] + atomicAdd(&lpos[g], 1u);
-        if (pos < cap) L0[(int64_t)w * cap + pos] = make_uint2((uint32_t)(ci.j0 + job_of<VEC>(t)), b);
+        if (pos < cap) L0[(int64_t)w * cap + pos] = make_uint2((uint32_t)(ci.j0 + job_of<VEC>(t)), cs.v[t][g]);
       }
     }
   }
@@ -537,9 +537,12 @@ __global__ __launch_bounds__(256) void sa_guess_hist_kernel(SegAuction a) {
   int32_t addk[kKG];
   uint32_t negbin = 0;
   bool low = false;  // some worker's bin holds -inf
+  bool any_bad = !a.lst;
   for (int g = 0; g < kKG; ++g) {
     addk[g] = -0x20000;
     if (g >= nw) continue;
+    if (a.lst && !a.lbad[hw0 + g]) continue;  // its list gave this round's threshold and bids: no values here
+    any_bad = true;
     const int32_t base = window_base(a.sel[(sw0 + g) * 4 + 2]);
     if (base >= 0x8000) {
       addk[g] = 0x8000 - base;
@@ -549,6 +552,7 @@ __global__ __launch_bounds__(256) void sa_guess_hist_kernel(SegAuction a) {
       low |= base < 0x400;
     }
   }
+  if (!any_bad) return;  // block-uniform
   ChunkScores cs;
   load_chunk<VEC>(a, ci, w0, cs);
   const LaneJobs lj = lane_jobs<VEC>(ci, cs);
@@ -667,6 +671,10 @@ __global__ __launch_bounds__(256) void sa_select_guess_kernel(SegAuction a) {
   const int w = (int)(hw % a.K);
   if (!(a.flag[s] & kLive)) return;
   const int lane = threadIdx.x & 63;
+  if (a.lst && !a.lbad[hw]) {  // threshold and bids from its list this round
+    if (lane == 0) a.miss[hw] = 0;
+    return;
+  }
   const uint32_t jpw = (uint32_t)((a.seg_off[s + 1] - a.seg_off[s]) / a.K);
   const uint32_t rank = jpw + 1;
   uint32_t* h = a.hist + hw * 256;
@@ -678,10 +686,6 @@ __global__ __launch_bounds__(256) void sa_select_guess_kernel(SegAuction a) {
   uint32_t b = 0, above = 0;
   if (hit) wave_select(h, rank - ab, b, above);
   if (lane == 0) {
-    // the bid list holds the keys >= T_prev - kListDelta: the new threshold must lie in that range
-    if (a.lst)
-      a.lbad[hw] = !hit || (int32_t)b < list_dmin(sel[2]) ||
-                   a.lcnt[hw * kAbovePad] > (uint32_t)a.lcs[hw / a.K];
     if (hit) {
       const uint32_t T = (uint32_t)window_base(sel[2]) + b;
       sel[0] = T >> 8;
@@ -1095,7 +1099,7 @@ __global__ __launch_bounds__(256) RQ_BID_ATTR void sa_bid_kernel(SegAuction a) {
     const int nwb = min(kKG, a.K - (int)blockIdx.y * kKG);
     bool bad = false;
     for (int g = 0; g < nwb; ++g) bad |= a.lbad[hwb + g] != 0;
-    if (!bad) return;  // (a block with one bad worker bids for all 16: the listed ones' keys are equal)
+    if (!bad) return;  // (in a block with a bad worker the listed workers bid nothing but retention keys)
   }
   __shared__ uint4 eqc[kKG][4];  // per (worker, wave): values equal to T in each job slice
   __shared__ uint32_t gneed[kKG], goff[kKG];
@@ -1109,10 +1113,12 @@ __global__ __launch_bounds__(256) RQ_BID_ATTR void sa_bid_kernel(SegAuction a) {
   _Float16 vT[kKG], vC[kKG];  // T and the comparison bound; NaN for workers past K (nothing bids)
   uint32_t need[kKG], off[kKG];
   uint32_t straddle = 0;
+  const bool listed = a.lst && !single;
   for (int g = 0; g < kKG; ++g) {
     vT[g] = vC[g] = __builtin_bit_cast(_Float16, (uint16_t)0x7E00u);
     need[g] = off[g] = 0;
     if (g >= nw) continue;
+    if (listed && !a.lbad[(int64_t)a.hidx[ci.s] * a.K + w0 + g]) continue;  // bids from its list (NaN: none here)
     const uint32_t kT = a.sel[(sw0 + g) * 4 + 2];
     need[g] = a.sel[(sw0 + g) * 4 + 3];
     vT[g] = vC[g] = __builtin_bit_cast(_Float16, okey_inv(kT));
@@ -1203,60 +1209,147 @@ __global__ __launch_bounds__(256) RQ_BID_ATTR void sa_bid_kernel(SegAuction a) {
     if (best[t] >> 16) atomicMax(&a.key[ci.j0 + job_of<VEC>(t)], best[t]);
 }
 
-// ---- the list pass (single auction): each worker's bids from its list, with the sweep's arithmetic ----
-// A value above T bids fp16(fp16(x - T) + eps); a value equal to T bids eps when it is among the first
-// `need` equal values in job order: all-or-none per chunk from the tie offsets (eqcnt / eqtot), and in the
-// one straddling chunk by its rank among the chunk's equal values (its list entries are one contiguous
-// range: one reservation per (chunk, worker)).  The retention (round < 100: the previous winner bids eps)
-// and leftover (round > 1000: worker 0 bids eps on jobs without a bidder) overrides apply to listed pairs
-// here; resolve adds them for pairs outside the lists.
-__global__ __launch_bounds__(256) void sa_list_bid_kernel(SegAuction a) {
-  const int64_t hw = blockIdx.y;
+// ---- list rounds ---------------------------------------------------------------------------------------
+// A round of a wide segment sweeps W twice (guessed pass, bids), although a worker's threshold T (its
+// (jpw+1)-th largest value) barely moves between rounds (median 0 keys, 99th percentile ~22 keys in an
+// oracle simulation of the candidate-fit shape).  So a sweep round also records, per worker, every job whose
+// value key is >= lkb = T_prev - kListDelta (with its raw score), and the following rounds run from that
+// list alone.  Values only fall between rounds (costs only rise), except that the previous winner's value is
+// its raw score; a worker wins a job only by bidding on it, i.e. from a listed value (or in a sweep round,
+// after which T >= lkb is checked).  So while a list round's threshold stays >= lkb (>= jpw + 1 listed values
+// at or above lkb), the list holds every value >= T and the round's selection, tie ranks and bids are the
+// sweep's exactly.  The leftover rounds (> 1000: worker 0 bids on jobs without a bidder, unlisted pairs)
+// sweep.  A worker whose list fails (none yet, T_prev < lkb, too few values, too many ties, overflow) takes
+// the sweep path this round (lbad = 1), which rebuilds its list.
+// One block per (segment, worker): values recomputed from raw score, cost and winner; the two-byte radix
+// select of the keys >= lkb; the jobs of the values equal to T sorted in LDS (their first `need` in job order
+// bid eps); bids, retention / leftover overrides and the packed atomicMax of the sweep.
+constexpr int kListEq = 2048;  // values equal to T a list round ranks in LDS (more: sweep)
+__global__ __launch_bounds__(256) void sa_list_round_kernel(SegAuction a) {
+  const int64_t hw = blockIdx.x;
   const int r = (int)(hw / a.K), w = (int)(hw % a.K);
   const int sg = a.mseg[r];
-  if (!(a.flag[sg] & kLive) || a.lbad[hw]) return;
-  const uint32_t cap = (uint32_t)a.lcs[r];
-  const uint32_t n = min(a.lcnt[hw * kAbovePad], cap);
+  if (!(a.flag[sg] & kLive)) return;
+  __shared__ uint32_t hst[256];
+  __shared__ uint32_t eqj[kListEq];
+  __shared__ uint32_t sh[4];  // bin, above, T, need | number of equal values
+  const int tid = threadIdx.x;
   const int counter = *a.round_dev;
+  const uint32_t cap = (uint32_t)a.lcs[r];
+  const uint32_t n = a.lcnt[hw * kAbovePad];
+  const uint32_t kb = a.lkb[hw];
+  const int64_t sw = (int64_t)sg * a.K + w;
+  const uint32_t jpw = (uint32_t)((a.seg_off[sg + 1] - a.seg_off[sg]) / a.K);
+  const uint2* L = a.lst + a.loff[r] + (int64_t)w * cap;
+  auto fail_list = [&]() {
+    if (tid == 0) {
+      a.lbad[hw] = 1;
+      a.lcnt[hw * kAbovePad] = 0;  // the sweep's guessed pass rebuilds it
+    }
+  };
+  if (n == 0 || n > cap || counter > 1000 || a.sel[sw * 4 + 2] < kb) return fail_list();
+  auto key_of = [&](const uint2 e) -> uint32_t {
+    return okey(value_bits(w, (uint16_t)e.y, a.hb[e.x], a.cost[e.x]));
+  };
+  hst[tid] = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += 256) {
+    const uint32_t k = key_of(L[i]);
+    if (k >= kb) atomicAdd(&hst[k >> 8], 1u);
+  }
+  __syncthreads();
+  if (tid < 64) {
+    uint32_t tot = hst[4 * tid] + hst[4 * tid + 1] + hst[4 * tid + 2] + hst[4 * tid + 3];
+    for (int o = 32; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o);
+    uint32_t b = 0, above = 0;
+    if (tot >= jpw + 1) wave_select(hst, jpw + 1, b, above);
+    if (tid == 0) {
+      sh[0] = tot >= jpw + 1 ? b : 0xFFFFFFFFu;
+      sh[1] = above;
+    }
+  }
+  __syncthreads();
+  const uint32_t b1 = sh[0];
+  if (b1 == 0xFFFFFFFFu) return fail_list();  // fewer than jpw + 1 values at or above the list base
+  hst[tid] = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += 256) {
+    const uint32_t k = key_of(L[i]);
+    if (k >= kb && (k >> 8) == b1) atomicAdd(&hst[k & 255u], 1u);
+  }
+  __syncthreads();
+  if (tid < 64) {
+    uint32_t b = 0, above = 0;
+    wave_select(hst, jpw + 1 - sh[1], b, above);
+    if (tid == 0) {
+      const uint32_t T = (b1 << 8) | b;
+      sh[2] = T;
+      sh[3] = jpw - (sh[1] + above);  // need: equal values that bid
+      sh[0] = 0;                      // equal values found (next pass)
+    }
+  }
+  __syncthreads();
+  const uint32_t T = sh[2], need = sh[3];
+  if (T < kb) return fail_list();  // (cannot happen with >= jpw + 1 values >= kb; kept as a guard)
+  // the jobs of the values equal to T, ascending
+  for (uint32_t i = tid; i < n; i += 256) {
+    const uint2 e = L[i];
+    if (key_of(e) == T) {
+      const uint32_t q = atomicAdd(&sh[0], 1u);
+      if (q < (uint32_t)kListEq) eqj[q] = e.x;
+    }
+  }
+  __syncthreads();
+  const uint32_t neq = sh[0];
+  if (neq > (uint32_t)kListEq) return fail_list();
+  uint32_t m = 1;
+  while (m < neq) m <<= 1;
+  for (uint32_t i = neq + tid; i < m; i += 256) eqj[i] = 0xFFFFFFFFu;
+  __syncthreads();
+  for (uint32_t kk = 2; kk <= m; kk <<= 1)  // bitonic sort of the equal values' jobs
+    for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+      for (uint32_t i = tid; i < m; i += 256) {
+        const uint32_t p = i ^ jj;
+        if (p > i) {
+          const uint32_t x = eqj[i], y = eqj[p];
+          if ((x > y) == ((i & kk) == 0)) {
+            eqj[i] = y;
+            eqj[p] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
   const uint16_t eps = a.eps[sg];
   const _Float16 epsh = __builtin_bit_cast(_Float16, eps);
-  const int64_t sw = (int64_t)sg * a.K + w;
-  const uint32_t kT = a.sel[sw * 4 + 2], need = a.sel[sw * 4 + 3];
-  const _Float16 vT = __builtin_bit_cast(_Float16, okey_inv(kT));
-  const uint32_t* e = a.eqcnt + (int64_t)w * a.total_chunks;
-  const uint32_t etot = a.eqtot[sw];
-  const int64_t j0 = a.seg_off[sg], c0 = a.chunk_off[sg], c_last = a.chunk_off[sg + 1] - 1;
-  const uint2* L = a.lst + a.loff[r] + (int64_t)w * cap;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const uint2 en = L[i];
-    const uint32_t j = en.x;
-    const _Float16 x = __builtin_bit_cast(_Float16, (uint16_t)en.y);
+  const _Float16 vT = __builtin_bit_cast(_Float16, okey_inv(T));
+  for (uint32_t i = tid; i < n; i += 256) {
+    const uint2 e = L[i];
+    const uint32_t j = e.x;
+    const int32_t hbj = a.hb[j];
+    const uint16_t xb = value_bits(w, (uint16_t)e.y, hbj, a.cost[j]);
+    const uint32_t k = okey(xb);
     uint32_t bid = 0;
-    if (x > vT) {
-      bid = __builtin_bit_cast(uint16_t, (_Float16)((_Float16)(x - vT) + epsh));
-    } else if (x == vT) {
-      const int64_t cl = ((int64_t)j - j0) / kCh, c = c0 + cl;
-      const uint32_t off = e[c], nc = (c < c_last ? e[c + 1] : etot) - off;
-      if (need >= off + nc) {
-        bid = eps;
-      } else if (need > off) {
-        uint32_t rank = 0;  // equal values of this chunk with a smaller job (the chunk's range around i)
-        for (uint32_t k = i; k-- > 0;) {
-          const uint2 o = L[k];
-          if (((int64_t)o.x - j0) / kCh != cl) break;
-          rank += __builtin_bit_cast(_Float16, (uint16_t)o.y) == vT && o.x < j;
-        }
-        for (uint32_t k = i + 1; k < n; ++k) {
-          const uint2 o = L[k];
-          if (((int64_t)o.x - j0) / kCh != cl) break;
-          rank += __builtin_bit_cast(_Float16, (uint16_t)o.y) == vT && o.x < j;
-        }
-        if (off + rank < need) bid = eps;
+    if (k > T) {
+      bid = __builtin_bit_cast(uint16_t, (_Float16)((_Float16)(__builtin_bit_cast(_Float16, xb) - vT) + epsh));
+    } else if (k == T && need) {
+      uint32_t lo = 0, hi = neq;  // rank of j among the equal values' jobs
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (eqj[mid] < j) lo = mid + 1; else hi = mid;
       }
+      if (lo < need) bid = eps;
     }
-    if (counter < 100 && a.hb[j] == w) bid = eps;
-    if (counter > 1000 && w == 0 && a.nobid[j]) bid = eps;
+    if (counter < 100 && hbj == w) bid = eps;  // retention: the previous winner bids eps on its job
     if (bid) atomicMax(&a.key[j], (bid << 16) | (0xFFFFu - (uint32_t)w));
+  }
+  if (tid == 0) {
+    uint32_t* sel = a.sel + sw * 4;
+    sel[0] = T >> 8;
+    sel[1] = 0;
+    sel[2] = T;
+    sel[3] = need;
+    a.lbad[hw] = 0;
   }
 }
 
@@ -1289,8 +1382,7 @@ __global__ __launch_bounds__(256) void sa_round_end_kernel(SegAuction a, int cou
     if (a.any_miss) *a.any_miss = 0;  // for the next round's select_guess (a store at the top of the guessed
                                       // pass would turn its uniform loads into vector loads)
   }
-  if (a.lst)
-    for (int64_t hw = s; hw < (int64_t)a.n_multi * a.K; hw += (int64_t)gridDim.x * 256) a.lcnt[hw * kAbovePad] = 0;
+
   uint32_t live = 0;
   if (s < a.S && (a.flag[s] & kLive)) {
     const int64_t n_s = a.n_glob ? a.n_glob : a.seg_off[s + 1] - a.seg_off[s];
@@ -1338,6 +1430,9 @@ __global__ __launch_bounds__(256) void sa_snapshot_kernel(SegAuction a, int32_t*
     if (!restore) a.s_sel[ns] = (uint32_t)*a.round_dev;
     else *a.round_dev = (int32_t)a.s_sel[ns];
   }
+  // a rollback raises values again (costs of the block's start): lists built inside the block are void
+  if (restore && a.lst)
+    for (int64_t hw = g0; hw < (int64_t)a.n_multi * a.K; hw += gs) a.lcnt[hw * kAbovePad] = 0;
 }
 
 // multi-chunk segment ranks (one block): hidx[s] = rank or -1, mseg[rank] = s; live_count[1] = total
@@ -1416,10 +1511,11 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   // the bid lists of the multi-chunk segments (RQSID_AUCTION_LIST=0: the sweep, for A/B): segment s holds
   // K * (4 * (N_s / K) + 256) <= 4 N_s + 256 K entries
   const char* el = getenv("RQSID_AUCTION_LIST");
-  const bool list = guess && a.n_multi > 0 && (int64_t)a.n_multi * K <= 65535 && !(el && !atoi(el));
+  const bool list = guess && a.n_multi > 0 && !(el && !atoi(el));
   const int64_t nm = a.n_multi > 0 ? a.n_multi : 1;
   a.lst = list ? c.take<uint2>(4 * N + 256 * (int64_t)K * nm) : nullptr;
   a.lcnt = list ? c.take<uint32_t>(nm * K * kAbovePad) : nullptr;
+  a.lkb = list ? c.take<uint32_t>(nm * K) : nullptr;
   a.lbad = list ? c.take<uint8_t>(nm * K) : nullptr;
   a.loff = list ? c.take<int64_t>(nm) : nullptr;
   a.lcs = list ? c.take<int32_t>(nm) : nullptr;
@@ -1532,8 +1628,6 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   // lean rounds leave out the two-pass kernels of missed workers (five launches of a few us each, empty
   // in most rounds); a lean block runs from a snapshot of the round state and is replayed with the full
   // rounds when any worker missed in it, so the result is the full rounds' in every case
-  // list pass grid: blocks per (segment, worker) for about twice the average list (~1.5 jobs per worker)
-  const unsigned lgx = (unsigned)std::min<int64_t>(std::max<int64_t>(cdiv(2 * n_jobs / std::max(1, n_multi) / n_workers, 256), 1), 16);
   if (a.lst) {
     if (hipMemsetAsync(a.lcnt, 0, (size_t)n_multi * n_workers * kAbovePad * 4, st) != hipSuccess ||
         hipMemsetAsync(a.lbad, 1, (size_t)n_multi * n_workers, st) != hipSuccess)
@@ -1541,6 +1635,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     hipLaunchKernelGGL(sa_list_layout_kernel, dim3(1), dim3(1), 0, st, a);
   }
   auto launch_round = [&](hipStream_t q, bool count, bool lean) {
+    if (a.lst) hipLaunchKernelGGL(sa_list_round_kernel, dim3((unsigned)(n_multi * a.K)), dim3(256), 0, q, a);
     if (n_multi > 0) {
       if (vec) hipLaunchKernelGGL((sa_guess_hist_kernel<true>), gcw, dim3(256), 0, q, a);
       else hipLaunchKernelGGL((sa_guess_hist_kernel<false>), gcw, dim3(256), 0, q, a);
@@ -1562,7 +1657,6 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     if (any_single) hipLaunchKernelGGL(sa_small_select_kernel, gcw, dim3(256), 0, q, a);
     if (vec) hipLaunchKernelGGL((sa_bid_kernel<true>), gcw, dim3(256), 0, q, a);
     else hipLaunchKernelGGL((sa_bid_kernel<false>), gcw, dim3(256), 0, q, a);
-    if (a.lst) hipLaunchKernelGGL(sa_list_bid_kernel, dim3(lgx, (unsigned)(n_multi * a.K)), dim3(256), 0, q, a);
     hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, q, a, out_assign);
     hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
   };
