@@ -1225,7 +1225,8 @@ __global__ __launch_bounds__(256) RQ_BID_ATTR void sa_bid_kernel(SegAuction a) {
 // select of the keys >= lkb; the jobs of the values equal to T sorted in LDS (their first `need` in job order
 // bid eps); bids, retention / leftover overrides and the packed atomicMax of the sweep.
 constexpr int kListEq = 2048;  // values equal to T a list round ranks in LDS (more: sweep)
-__global__ __launch_bounds__(256) void sa_list_round_kernel(SegAuction a) {
+constexpr int kLT = 1024;  // threads of a list-round block
+__global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
   const int64_t hw = blockIdx.x;
   const int r = (int)(hw / a.K), w = (int)(hw % a.K);
   const int sg = a.mseg[r];
@@ -1240,7 +1241,7 @@ __global__ __launch_bounds__(256) void sa_list_round_kernel(SegAuction a) {
   const uint32_t kb = a.lkb[hw];
   const int64_t sw = (int64_t)sg * a.K + w;
   const uint32_t jpw = (uint32_t)((a.seg_off[sg + 1] - a.seg_off[sg]) / a.K);
-  const uint2* L = a.lst + a.loff[r] + (int64_t)w * cap;
+  uint2* const L = a.lst + a.loff[r] + (int64_t)w * cap;
   auto fail_list = [&]() {
     if (tid == 0) {
       a.lbad[hw] = 1;
@@ -1248,13 +1249,14 @@ __global__ __launch_bounds__(256) void sa_list_round_kernel(SegAuction a) {
     }
   };
   if (n == 0 || n > cap || counter > 1000 || a.sel[sw * 4 + 2] < kb) return fail_list();
-  auto key_of = [&](const uint2 e) -> uint32_t {
-    return okey(value_bits(w, (uint16_t)e.y, a.hb[e.x], a.cost[e.x]));
-  };
-  hst[tid] = 0;
+  if (tid < 256) hst[tid] = 0;
   __syncthreads();
-  for (uint32_t i = tid; i < n; i += 256) {
-    const uint32_t k = key_of(L[i]);
+  // pass 1: this round's value keys (raw score, cost, last winner), kept in the entries' upper 16 bits so
+  // the later passes read the list only
+  for (uint32_t i = tid; i < n; i += kLT) {
+    const uint2 e = L[i];
+    const uint32_t k = okey(value_bits(w, (uint16_t)e.y, a.hb[e.x], a.cost[e.x]));
+    L[i].y = (e.y & 0xFFFFu) | (k << 16);
     if (k >= kb) atomicAdd(&hst[k >> 8], 1u);
   }
   __syncthreads();
@@ -1271,10 +1273,11 @@ __global__ __launch_bounds__(256) void sa_list_round_kernel(SegAuction a) {
   __syncthreads();
   const uint32_t b1 = sh[0];
   if (b1 == 0xFFFFFFFFu) return fail_list();  // fewer than jpw + 1 values at or above the list base
-  hst[tid] = 0;
   __syncthreads();
-  for (uint32_t i = tid; i < n; i += 256) {
-    const uint32_t k = key_of(L[i]);
+  if (tid < 256) hst[tid] = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += kLT) {
+    const uint32_t k = L[i].y >> 16;
     if (k >= kb && (k >> 8) == b1) atomicAdd(&hst[k & 255u], 1u);
   }
   __syncthreads();
@@ -1291,12 +1294,14 @@ __global__ __launch_bounds__(256) void sa_list_round_kernel(SegAuction a) {
   __syncthreads();
   const uint32_t T = sh[2], need = sh[3];
   if (T < kb) return fail_list();  // (cannot happen with >= jpw + 1 values >= kb; kept as a guard)
-  // the jobs of the values equal to T, ascending
-  for (uint32_t i = tid; i < n; i += 256) {
-    const uint2 e = L[i];
-    if (key_of(e) == T) {
-      const uint32_t q = atomicAdd(&sh[0], 1u);
-      if (q < (uint32_t)kListEq) eqj[q] = e.x;
+  // the jobs of the values equal to T, ascending (only `need` of them bid; none when need == 0)
+  if (need) {
+    for (uint32_t i = tid; i < n; i += kLT) {
+      const uint2 e = L[i];
+      if ((e.y >> 16) == T) {
+        const uint32_t q = atomicAdd(&sh[0], 1u);
+        if (q < (uint32_t)kListEq) eqj[q] = e.x;
+      }
     }
   }
   __syncthreads();
@@ -1304,11 +1309,11 @@ __global__ __launch_bounds__(256) void sa_list_round_kernel(SegAuction a) {
   if (neq > (uint32_t)kListEq) return fail_list();
   uint32_t m = 1;
   while (m < neq) m <<= 1;
-  for (uint32_t i = neq + tid; i < m; i += 256) eqj[i] = 0xFFFFFFFFu;
+  for (uint32_t i = neq + tid; i < m; i += kLT) eqj[i] = 0xFFFFFFFFu;
   __syncthreads();
   for (uint32_t kk = 2; kk <= m; kk <<= 1)  // bitonic sort of the equal values' jobs
     for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-      for (uint32_t i = tid; i < m; i += 256) {
+      for (uint32_t i = tid; i < m; i += kLT) {
         const uint32_t p = i ^ jj;
         if (p > i) {
           const uint32_t x = eqj[i], y = eqj[p];
@@ -1323,15 +1328,14 @@ __global__ __launch_bounds__(256) void sa_list_round_kernel(SegAuction a) {
   const uint16_t eps = a.eps[sg];
   const _Float16 epsh = __builtin_bit_cast(_Float16, eps);
   const _Float16 vT = __builtin_bit_cast(_Float16, okey_inv(T));
-  for (uint32_t i = tid; i < n; i += 256) {
+  const bool ret = counter < 100;
+  for (uint32_t i = tid; i < n; i += kLT) {
     const uint2 e = L[i];
-    const uint32_t j = e.x;
-    const int32_t hbj = a.hb[j];
-    const uint16_t xb = value_bits(w, (uint16_t)e.y, hbj, a.cost[j]);
-    const uint32_t k = okey(xb);
+    const uint32_t j = e.x, k = e.y >> 16;
     uint32_t bid = 0;
     if (k > T) {
-      bid = __builtin_bit_cast(uint16_t, (_Float16)((_Float16)(__builtin_bit_cast(_Float16, xb) - vT) + epsh));
+      const _Float16 x = __builtin_bit_cast(_Float16, okey_inv(k));
+      bid = __builtin_bit_cast(uint16_t, (_Float16)((_Float16)(x - vT) + epsh));
     } else if (k == T && need) {
       uint32_t lo = 0, hi = neq;  // rank of j among the equal values' jobs
       while (lo < hi) {
@@ -1340,7 +1344,7 @@ __global__ __launch_bounds__(256) void sa_list_round_kernel(SegAuction a) {
       }
       if (lo < need) bid = eps;
     }
-    if (counter < 100 && hbj == w) bid = eps;  // retention: the previous winner bids eps on its job
+    if (ret && a.hb[j] == w) bid = eps;  // retention: the previous winner bids eps on its job
     if (bid) atomicMax(&a.key[j], (bid << 16) | (0xFFFFu - (uint32_t)w));
   }
   if (tid == 0) {
@@ -1635,7 +1639,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     hipLaunchKernelGGL(sa_list_layout_kernel, dim3(1), dim3(1), 0, st, a);
   }
   auto launch_round = [&](hipStream_t q, bool count, bool lean) {
-    if (a.lst) hipLaunchKernelGGL(sa_list_round_kernel, dim3((unsigned)(n_multi * a.K)), dim3(256), 0, q, a);
+    if (a.lst) hipLaunchKernelGGL(sa_list_round_kernel, dim3((unsigned)(n_multi * a.K)), dim3(kLT), 0, q, a);
     if (n_multi > 0) {
       if (vec) hipLaunchKernelGGL((sa_guess_hist_kernel<true>), gcw, dim3(256), 0, q, a);
       else hipLaunchKernelGGL((sa_guess_hist_kernel<false>), gcw, dim3(256), 0, q, a);
