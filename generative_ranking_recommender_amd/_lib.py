@@ -19,7 +19,7 @@ PKG = Path(__file__).resolve().parent
 REPO = PKG.parent
 LIB_PATH = PKG / "librqsid.so"
 SRCS = [PKG / "csrc" / "rqsid.hip", PKG / "csrc" / "assign.hip", PKG / "csrc" / "assign_stream.hip",
-        PKG / "csrc" / "assign_resident.hip", PKG / "csrc" / "auction.hip",
+        PKG / "csrc" / "assign_resident.hip", PKG / "csrc" / "assign_rows.hip", PKG / "csrc" / "auction.hip",
         PKG / "csrc" / "auction_seg.hip"]
 DEPS = SRCS + [PKG / "csrc" / "internal.h", PKG / "csrc" / "assign_common.h"]
 HEADER = REPO / "include" / "rqsid.h"

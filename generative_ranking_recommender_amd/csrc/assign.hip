@@ -1338,7 +1338,9 @@ void set_attrs(bool* ok) {
 
 // screen variant (tuning / A-B tests): 0 default (per level: see rqsid_assign); 1: per-tile kernel
 // only; 2: per-tile kernel with the multi-sweep list epilogue on single-pass segments; 5: the
-// persistent streamed kernels (assign_stream.hip, RQSID_STREAM_SHAPE) where they apply
+// persistent streamed kernels (assign_stream.hip, RQSID_STREAM_SHAPE) where they apply; 6: the
+// centre-resident screen; 7: no candidate split; 8: the row-resident screen (assign_rows.hip,
+// RQSID_ROWS_SHAPE)
 int screen_variant() {  // read per call: tests switch it within one process
   const char* e = getenv("RQSID_SCREEN_VARIANT");
   return e ? atoi(e) : 0;
@@ -1513,7 +1515,14 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   const bool res_ok = resident_supported(dim, cand_count_max, t3, res_levels) && (int64_t)n_segments + 1 <= n_rows &&
                       (res_levels != 1 || !norm || den_out);
   const bool use_res = res_ok && variant == 6;
-  if (use_res) {
+  // the row-resident screen (assign_rows.hip): variant 8 forces it wherever it applies (1-term levels of
+  // 512-d rows with <= 512 candidates)
+  const bool use_rows = variant == 8 && rows_supported(dim, cand_count_max, t3, res_levels, norm) &&
+                        (int64_t)n_segments + 1 <= n_rows;
+  if (use_rows) {
+    // R-row tile offsets in the compact-list area, the tile map in the tile_seg slot; compact work list
+    if ((rc = launch_rows_screen(p, res_levels, norm, tile_seg, work_idx, n_rows, st))) return rc;
+  } else if (use_res) {
     p.err = p.work_count + 48;  // zeroed with the workspace header above
     const char* fc = getenv("RQSID_TEST_FORCE_SPIN_CAP");
     p.force_cap = fc && atoi(fc) ? 1 : 0;
@@ -1546,7 +1555,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   // candidates, 1-term <= 512 (the XL preset's middle and last levels); RQSID_SCREEN_VARIANT=7 (or 2)
   // keeps the multi-pass screen for comparison
   const bool split = !legacy && variant != 7 && dim <= kSplitDim;
-  if (use_stream || use_res) {
+  if (use_stream || use_res || use_rows) {
   } else if (t3 && cand_count_max > 128 && split) launch_screen<4, kSplitS, true, true, 2>(p, res_levels, norm, grid, st);
   else if (t3) launch_screen2<4, 2, true>(p, res_levels, norm, grid, !legacy && cand_count_max <= 128, st);
   else if (cand_count_max <= 128) launch_screen2<4, 2, false>(p, res_levels, norm, grid, !legacy, st);

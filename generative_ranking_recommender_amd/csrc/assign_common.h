@@ -477,6 +477,13 @@ __device__ __forceinline__ void row_frag(const float4 xa, const float4 xc, const
 int launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
                          int32_t* seg_tile256, int64_t cap, int shape, hipStream_t st);
 bool stream_supported(int nt, bool t3, int rl, bool norm);
+// R-row tiling of the segments on the device: seg_tiles[s] (n_segments + 1 ints) and tile -> segment
+// (tile_seg, cap / R + n_segments entries at most)
+void launch_tiling(const AssignParams& p, int R, int32_t* tile_seg, int32_t* seg_tiles, int64_t cap, hipStream_t st);
+// row-resident screen (assign_rows.hip): 512-d rows, 1 term, <= 512 candidates per segment
+bool rows_supported(int dim, int cand_count_max, bool t3, int rl, bool norm);
+int launch_rows_screen(const AssignParams& p, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles, int64_t cap,
+                       hipStream_t st);
 
 // centre-resident screen (assign_resident.hip): 512-d rows, <= 256 candidates per segment (1 term) or
 // <= 128 (3 terms).  desc: resident_desc_bytes(n_rows) of workspace; seg_tile32: n_segments + 1 ints.

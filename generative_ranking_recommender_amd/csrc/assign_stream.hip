@@ -1239,6 +1239,13 @@ bool stream_supported(int nt, bool t3, int rl, bool norm) {
   return false;
 }
 
+void launch_tiling(const AssignParams& p, int R, int32_t* tile_seg, int32_t* seg_tiles, int64_t cap, hipStream_t st) {
+  hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, R, seg_tiles);
+  const int64_t max_tiles = cap / R + p.n_segments;
+  const unsigned tg = (unsigned)(max_tiles / 256 + 1 < 4096 ? max_tiles / 256 + 1 : 4096);
+  hipLaunchKernelGGL(tile_seg_kernel, dim3(tg), dim3(256), 0, st, seg_tiles, p.n_segments, cap, tile_seg);
+}
+
 int launch_stream_screen(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg,
                          int32_t* seg_tiles, int64_t cap, int shape, hipStream_t st) {
   if (shape == 0) shape = stream_shape();
