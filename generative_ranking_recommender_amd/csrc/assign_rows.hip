@@ -97,6 +97,7 @@ __global__ __launch_bounds__(W * 64, 2) void assign_rows_kernel(AssignParams p, 
     const bool flag = p.seg_flags && (__builtin_amdgcn_readfirstlane(p.seg_flags[s]) & RQSID_SEG_PENALTY);
     const int my_local = wave * 32 + r;
     const bool row_valid = my_local < nrows;
+    const bool wave_live = wave * 32 < nrows;
     const int pos = t0 + (row_valid ? my_local : 0);
     const int my_row = p.row_index ? p.row_index[pos] : pos;
     __syncthreads();  // the previous tile's LDS (ring, meta, candidate ids, residual rows) is consumed
@@ -274,6 +275,15 @@ __global__ __launch_bounds__(W * 64, 2) void assign_rows_kernel(AssignParams p, 
       f32x16 acc[NTB];
 #pragma unroll
       for (int t = 0; t < NTB; ++t) acc[t] = zero16;
+      if (!wave_live) {  // a wave past the tile's rows keeps the ring's waits and DMAs, computes nothing
+#pragma unroll
+        for (int c = 0; c < kRNch; ++c) {
+          const int q = blk * kRNch + c;
+          wait_chunks<S, P>(min(S - 2, NQ - 1 - q));
+          if (q + S - 1 < NQ) issue(q + S - 1);
+        }
+        continue;
+      }
 #pragma unroll
       for (int c = 0; c < kRNch; ++c) {
         const int q = blk * kRNch + c;
@@ -364,6 +374,7 @@ __global__ __launch_bounds__(W * 64, 2) void assign_rows_kernel(AssignParams p, 
         }
       }
     }
+    if (!wave_live) continue;
     // row decision (assign_screen_kernel's multi-pass form): the listed candidates still within the final
     // U; an overflowing half, a non-finite bound or no candidate -> re-score every candidate
     const float Uf = fmaf(fabsf(U), 0x1p-22f, U) + 1.2e-38f;
