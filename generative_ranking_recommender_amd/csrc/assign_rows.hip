@@ -448,13 +448,13 @@ bool launch_rows_one(const AssignParams& p, const int32_t* tile_seg, const int32
   return true;
 }
 
-// block shape: RQSID_ROWS_SHAPE = 44 (4 waves x 4 ring stages, two blocks per CU: one block's row loads
-// overlap the other's MFMAs; the default) or 88 (8 waves x 8 stages, one block per CU: half the centre
-// bytes per row, the row loads exposed)
+// block shape RQSID_ROWS_SHAPE = 10 W + S: 48 (4 waves, 8 ring stages, two blocks per CU: one block's row
+// loads overlap the other's MFMAs; the default), 44 (4 stages) or 88 (8 waves, one block per CU: half the
+// centre bytes per row, row loads exposed)
 int rows_shape() {
   const char* e = getenv("RQSID_ROWS_SHAPE");
-  const int v = e ? atoi(e) : 44;
-  return v == 88 ? 88 : 44;
+  const int v = e ? atoi(e) : 48;
+  return v == 44 || v == 88 ? v : 48;
 }
 
 template <int W, int S>
@@ -476,10 +476,11 @@ bool rows_supported(int dim, int cand_count_max, bool t3, int rl, bool norm) {
 int launch_rows_screen(const AssignParams& p, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles, int64_t cap,
                        hipStream_t st) {
   const int shape = rows_shape();
-  const int R = shape == 44 ? 128 : 256;
+  const int R = shape == 88 ? 256 : 128;
   launch_tiling(p, R, tile_seg, seg_tiles, cap, st);
-  const bool ok = shape == 44 ? launch_rows_w<4, 4>(p, rl, norm, tile_seg, seg_tiles, st)
-                              : launch_rows_w<8, 8>(p, rl, norm, tile_seg, seg_tiles, st);
+  const bool ok = shape == 88   ? launch_rows_w<8, 8>(p, rl, norm, tile_seg, seg_tiles, st)
+                  : shape == 44 ? launch_rows_w<4, 4>(p, rl, norm, tile_seg, seg_tiles, st)
+                                : launch_rows_w<4, 8>(p, rl, norm, tile_seg, seg_tiles, st);
   return ok ? RQSID_OK : fail(RQSID_E_LAUNCH, "assign: row-resident screen launch failed (device query / LDS attribute)");
 }
 
