@@ -29,17 +29,12 @@ constexpr int kRMaxCand = 512;    // candidates per segment
 #define RQSID_ROWS_NTB 2
 #endif
 constexpr int kNTB = RQSID_ROWS_NTB;  // MFMA tiles (32 candidates) per candidate block
-#ifndef RQSID_ROWS_BCH
-#define RQSID_ROWS_BCH 1
-#endif
-constexpr int kBCH = RQSID_ROWS_BCH;  // row chunks per load batch (two batches in flight)
-
-template <int W, int S, int BCH, int NTB>
+template <int W, int S, int SR, int NTB>
 struct RowsLayout {
   static constexpr int kCB = NTB * 32;                // candidates per block (NTB MFMA tiles of 32)
   static constexpr int kCStage = kCB * 64;            // kCB candidates x 32 fp16 dims (hi terms)
-  static constexpr int kScr = S * kCStage;            // per-wave transpose scratch: BCH chunks x 32 rows x 64 B
-  static constexpr int kScrWave = BCH * 32 * 64;
+  static constexpr int kScr = S * kCStage;            // per-wave row rings: SR stages x 32 rows x 128 B (fp32)
+  static constexpr int kScrWave = SR * 32 * 128;
   static constexpr int kMeta = kScr + W * kScrWave;   // |c|^2 [512], |c| [512]
   static constexpr int kGidx = kMeta + 2 * kRMaxCand * 4;  // global centre of each local candidate [512]
   static constexpr int kRes = kGidx + kRMaxCand * 4;  // residual centre rows ca, cb (fp32 512 each)
@@ -49,16 +44,23 @@ struct RowsLayout {
   static constexpr int P = kOps >= W ? kOps / W : 1;  // per issuing wave (waves >= kOps / P issue none)
   static_assert(kOps % W == 0 || W % kOps == 0, "centre DMA split");
   static_assert(kRNch % S == 0, "ring stages must divide the chunks of a block (static stage index)");
-  static_assert(kRNch % (2 * BCH) == 0, "row batches (two in flight)");
+  static_assert(SR >= 2 && SR <= 4, "row ring depth");
   static_assert((S - 2) * P <= 63, "vmcnt field");
   static_assert(kBytes * kBlocks <= 160 * 1024, "LDS budget");
 };
 
-template <int W, int S, int BCH, int NTB, int RL, bool NORM>
+// wait until at most 4*younger vector-memory ops of this wave are outstanding, then drain its LDS ops
+__device__ __forceinline__ void wait_rows(int younger) {
+  if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <int W, int S, int SR, int NTB, int RL, bool NORM>
 __global__ __launch_bounds__(W * 64, 2) void assign_rows_kernel(AssignParams p, const int32_t* __restrict__ tile_seg,
                                                                 const int32_t* __restrict__ seg_tiles) {
   static_assert(!(RL == 1 && NORM), "the first-residual normalising level writes den_out: per-tile kernel");
-  using L = RowsLayout<W, S, BCH, NTB>;
+  using L = RowsLayout<W, S, SR, NTB>;
   constexpr int P = L::P, R = W * 32, kCB = L::kCB;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 6, 2), 0");  // fp16/fp64 denormals flushed (to_f16)
@@ -81,7 +83,8 @@ __global__ __launch_bounds__(W * 64, 2) void assign_rows_kernel(AssignParams p, 
   int* const gidx = reinterpret_cast<int*>(smem + L::kGidx);
   float* const lds_ca = reinterpret_cast<float*>(smem + L::kRes);
   float* const lds_cb = lds_ca + kRDim;
-  unsigned char* const scr = smem + L::kScr + wave * L::kScrWave;
+  const unsigned char* const xring = smem + L::kScr + wave * L::kScrWave;
+  const int xsw = (r >> 1) & 7;  // swizzle of this lane's row in the x image
   const int csw = (r >> 2) & 3;  // swizzle of this lane's candidate row in the centre image
   const f32x16 zero16 = {};
 
@@ -100,6 +103,11 @@ __global__ __launch_bounds__(W * 64, 2) void assign_rows_kernel(AssignParams p, 
     const bool wave_live = wave * 32 < nrows;
     const int pos = t0 + (row_valid ? my_local : 0);
     const int my_row = p.row_index ? p.row_index[pos] : pos;
+    // the row's level-1 divisor, consumed here: a plain load still in flight when the row DMAs start would
+    // make hipcc drain them with vmcnt(0) at its first use
+    float inv1 = 1.0f;
+    if (RL >= 2 && NORM) inv1 = 1.0f / p.den_in[my_row];
+    asm volatile("" : "+v"(inv1));
     __syncthreads();  // the previous tile's LDS (ring, meta, candidate ids, residual rows) is consumed
     if (flag || cnt <= 0) {  // block-uniform
       WorkItem w{};
@@ -149,103 +157,57 @@ __global__ __launch_bounds__(W * 64, 2) void assign_rows_kernel(AssignParams p, 
       if (q < NQ) issue(q);
 
     // ---- rows -> residual -> fp16 B operand, resident for the tile ----------------------------------
-    // load layout: instruction i moves rows 8i + lane/8 (of this wave's 32), 16 B at dims 4*(lane%8) of a
-    // chunk; fragment layout: lane (r, h) holds dims 16 ks + 8 h .. +7 of row r for every k-step ks
-    int grow[4];
-    float inv1[4];
-    float se2[4], sf2[4];
+    // the wave's 32 rows stream chunk by chunk through its own SR-stage LDS-DMA ring (fp32 image: row rr at
+    // rr*128 B, 16-B slot q stored at q ^ ((rr>>1)&7); instruction i moves rows 8i + lane/8, 8 lanes per
+    // 128-B row line, the non-temporal hint) and row_frag turns each chunk into the B operand and the
+    // bound's sums, exactly as in the per-tile screen.  The ring is private to the wave: vmcnt alone orders it.
+    const float* xsrc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int lr = 8 * i + (lane >> 3);
-      grow[i] = __shfl(my_row, lr);
-      inv1[i] = (RL >= 2 && NORM) ? 1.0f / p.den_in[grow[i]] : 1.0f;
-      se2[i] = 0.f;
-      sf2[i] = 0.f;
+      const int rr = 8 * i + (lane >> 3);
+      const int grow = __shfl(my_row, rr);
+      xsrc[i] = p.x + (int64_t)grow * kRDim + ((lane & 7) ^ ((rr >> 1) & 7)) * 4;
     }
-    const int q8 = lane & 7;
+    const uint32_t rbase = lds0 + (uint32_t)(L::kScr + wave * L::kScrWave);
+    auto issue_rows = [&](int c) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        dma16_nt(xsrc[i] + c * 32, __builtin_amdgcn_readfirstlane(rbase + (uint32_t)((c % SR) * 4096 + i * 1024)));
+    };
+    RowSums rs;
     f16x8 bf[2 * kRNch];
-    typedef __attribute__((ext_vector_type(4))) float v4;
-    // two batches of BCH chunks in flight: batch b+1's loads are issued before batch b is converted
-    auto load = [&](v4 (&xv)[BCH][4], int c0) {
+    // this lane's half of the residual centre rows, as opaque bases: the per-chunk offsets then fold into the
+    // ds_read immediates (hipcc otherwise turns base + 8h + d into ORs of disjoint bits, materialises every
+    // chunk's address and spills them)
+    typedef __attribute__((address_space(3))) const float lds_f32;
+    lds_f32* ca3 = (lds_f32*)(lds_ca + 8 * h);  // pinned as LDS pointers (a pinned generic pointer
+    lds_f32* cb3 = (lds_f32*)(lds_cb + 8 * h);  // would turn the reads into flat loads, which count on vmcnt)
+    asm volatile("" : "+v"(ca3), "+v"(cb3));
+    const float* ca_h = (const float*)ca3;
+    const float* cb_h = (const float*)cb3;
 #pragma unroll
-      for (int bc = 0; bc < BCH; ++bc)
+    for (int c = 0; c < SR - 1; ++c) issue_rows(c);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          xv[bc][i] = __builtin_nontemporal_load(
-              reinterpret_cast<const v4*>(p.x + (int64_t)grow[i] * kRDim + (c0 + bc) * 32 + 4 * q8));
-    };
-    auto convert = [&](const v4 (&xv)[BCH][4], int c0) {
+    for (int c = 0; c < kRNch; ++c) {
+      __builtin_amdgcn_sched_barrier(0);  // one chunk at a time (hoisting every chunk's reads spills)
+      wait_rows(min(SR - 2, kRNch - 1 - c));  // chunk c landed; the stage chunk c-1 used is read
+      if (c + SR - 1 < kRNch) issue_rows(c + SR - 1);
+      const unsigned char* xb = xring + (c % SR) * 4096 + r * 128;
 #pragma unroll
-      for (int bc = 0; bc < BCH; ++bc) {
-        const int d0 = (c0 + bc) * 32 + 4 * q8;
-        float4 a4 = make_float4(0.f, 0.f, 0.f, 0.f), b4 = a4;
-        if (RL >= 1) a4 = *reinterpret_cast<const float4*>(lds_ca + d0);
-        if (RL >= 2) b4 = *reinterpret_cast<const float4*>(lds_cb + d0);
-        const float av[4] = {a4.x, a4.y, a4.z, a4.w}, bv[4] = {b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float v[4] = {xv[bc][i].x, xv[bc][i].y, xv[bc][i].z, xv[bc][i].w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (RL >= 1) v[e] = v[e] - av[e];  // the reference's fp32 operation sequence (row_frag)
-            if (RL >= 2) v[e] = (NORM ? v[e] * inv1[i] : v[e]) - bv[e];
-          }
-          const h2 lo = __builtin_convertvector(f2{v[0], v[1]}, h2);
-          const h2 hi = __builtin_convertvector(f2{v[2], v[3]}, h2);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float ex = v[e] - (float)(e < 2 ? lo[e] : hi[e - 2]);  // exact: the fp16 rounding residual
-            se2[i] = fmaf(ex, ex, se2[i]);
-            sf2[i] = fmaf(v[e], v[e], sf2[i]);
-          }
-          // scratch row lr at lr*64 B (32 fp16 dims), 16-B slot q stored at q ^ ((lr>>2)&3)
-          const int lr = 8 * i + (lane >> 3);
-          typedef __attribute__((ext_vector_type(4))) _Float16 h4;
-          const h4 hv = __builtin_shufflevector(lo, hi, 0, 1, 2, 3);
-          *reinterpret_cast<h4*>(scr + bc * 2048 + lr * 64 + (((q8 >> 1) ^ ((lr >> 2) & 3)) << 4) + (q8 & 1) * 8) = hv;
-        }
+      for (int ks = 0; ks < 2; ++ks) {
+        const int q0 = 4 * ks + 2 * h;
+        const float4 xa = *reinterpret_cast<const float4*>(xb + ((q0 ^ xsw) << 4));
+        const float4 xc = *reinterpret_cast<const float4*>(xb + (((q0 + 1) ^ xsw) << 4));
+        f16x8 bl;
+        row_frag<RL, NORM, false, true>(xa, xc, ca_h, cb_h, c * 32 + 16 * ks, inv1, bf[2 * c + ks], bl, rs);
       }
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int bc = 0; bc < BCH; ++bc)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-          bf[2 * (c0 + bc) + ks] =
-              *reinterpret_cast<const f16x8*>(scr + bc * 2048 + r * 64 + (((2 * ks + h) ^ ((r >> 2) & 3)) << 4));
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("" ::: "memory");
-    };
-    {
-      v4 xa[BCH][4], xb[BCH][4];
-      load(xa, 0);
-#pragma unroll
-      for (int c0 = 0; c0 < kRNch; c0 += 2 * BCH) {
-        load(xb, c0 + BCH);
-        convert(xa, c0);
-        if (c0 + 2 * BCH < kRNch) load(xa, c0 + 2 * BCH);
-        convert(xb, c0 + BCH);
-      }
-    }
-    // row sums: the 8 lanes of a row line -> every lane; then lane (r, h) takes row r's
-    float e2r = 0.f, f2r = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float a = se2[i], b = sf2[i];
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
-        a += __shfl_xor(a, o);
-        b += __shfl_xor(b, o);
-      }
-      const float ar = __shfl(a, (r & 7) * 8), br = __shfl(b, (r & 7) * 8);
-      e2r = (r >> 3) == i ? ar : e2r;
-      f2r = (r >> 3) == i ? br : f2r;
     }
     // bound constants of the row (assign_screen_kernel's pass-0 block, 1 term)
-    const float en = sqrtf(e2r) * 1.001f + 1e-30f;
+    const float se2 = rs.se2v.x + rs.se2v.y, sf2 = rs.sf2v.x + rs.sf2v.y;
+    const float en = sqrtf(se2 + __shfl_xor(se2, 32)) * 1.001f + 1e-30f;
     float inv_den = 1.f, dr = 0.f;
-    const float nrm = sqrtf(f2r);
-    if (NORM && RL >= 1) {  // RL 2: fp32 sums, |nrm - |v|| <= den_eps |v| (chains of <= dim/8 + 3 terms)
+    const float nrm = sqrtf(sf2 + __shfl_xor(sf2, 32));
+    if (NORM && RL >= 1) {  // RL 2: fp32 sums, |nrm - |v|| <= den_eps |v| (chains of dim/4 + 2 terms)
       const float den = nrm + 1e-8f;
       inv_den = 1.0f / den;
       const float den_eps = (0.125f * (float)kRDim + 3.0f) * 5.97e-8f;
@@ -430,40 +392,40 @@ __global__ __launch_bounds__(W * 64, 2) void assign_rows_kernel(AssignParams p, 
   }
 }
 
-template <int W, int S, int BCH, int NTB, int RL, bool NORM>
+template <int W, int S, int SR, int NTB, int RL, bool NORM>
 bool launch_rows_one(const AssignParams& p, const int32_t* tile_seg, const int32_t* seg_tiles, hipStream_t st) {
-  using L = RowsLayout<W, S, BCH, NTB>;
+  using L = RowsLayout<W, S, SR, NTB>;
   static bool attr[kMaxDevices] = {};
   const int dev = current_device(), ncu = device_cu_count();
   if (dev < 0 || !ncu) return false;
   if (!attr[dev]) {
-    if (hipFuncSetAttribute((const void*)assign_rows_kernel<W, S, BCH, NTB, RL, NORM>,
+    if (hipFuncSetAttribute((const void*)assign_rows_kernel<W, S, SR, NTB, RL, NORM>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, L::kBytes) != hipSuccess)
       return false;
     attr[dev] = true;
   }
   const int64_t g = (int64_t)ncu * L::kBlocks / 8 * 8;  // persistent: every block resident at once
-  hipLaunchKernelGGL((assign_rows_kernel<W, S, BCH, NTB, RL, NORM>), dim3((unsigned)(g < 8 ? 8 : g)), dim3(W * 64),
+  hipLaunchKernelGGL((assign_rows_kernel<W, S, SR, NTB, RL, NORM>), dim3((unsigned)(g < 8 ? 8 : g)), dim3(W * 64),
                      L::kBytes, st, p, tile_seg, seg_tiles);
   return true;
 }
 
-// block shape RQSID_ROWS_SHAPE = 10 W + S: 48 (4 waves, 8 ring stages, two blocks per CU: one block's row
-// loads overlap the other's MFMAs; the default), 44 (4 stages) or 88 (8 waves, one block per CU: half the
-// centre bytes per row, row loads exposed)
+// block shape RQSID_ROWS_SHAPE = 100 W + 10 S + SR (waves, centre ring stages, per-wave row ring stages):
+// 443 (the default) and 482: 4 waves, two blocks per CU (one block's row stream overlaps the other's
+// MFMAs); 883: 8 waves, one block per CU (half the centre bytes per row, the row stream exposed)
 int rows_shape() {
   const char* e = getenv("RQSID_ROWS_SHAPE");
-  const int v = e ? atoi(e) : 48;
-  return v == 44 || v == 88 ? v : 48;
+  const int v = e ? atoi(e) : 443;
+  return v == 482 || v == 883 ? v : 443;
 }
 
-template <int W, int S>
+template <int W, int S, int SR>
 bool launch_rows_w(const AssignParams& p, int rl, bool norm, const int32_t* tile_seg, const int32_t* seg_tiles,
                    hipStream_t st) {
-  if (rl == 0) return launch_rows_one<W, S, kBCH, kNTB, 0, false>(p, tile_seg, seg_tiles, st);
-  if (rl == 1) return !norm && launch_rows_one<W, S, kBCH, kNTB, 1, false>(p, tile_seg, seg_tiles, st);
-  if (norm) return launch_rows_one<W, S, kBCH, kNTB, 2, true>(p, tile_seg, seg_tiles, st);
-  return launch_rows_one<W, S, kBCH, kNTB, 2, false>(p, tile_seg, seg_tiles, st);
+  if (rl == 0) return launch_rows_one<W, S, SR, kNTB, 0, false>(p, tile_seg, seg_tiles, st);
+  if (rl == 1) return !norm && launch_rows_one<W, S, SR, kNTB, 1, false>(p, tile_seg, seg_tiles, st);
+  if (norm) return launch_rows_one<W, S, SR, kNTB, 2, true>(p, tile_seg, seg_tiles, st);
+  return launch_rows_one<W, S, SR, kNTB, 2, false>(p, tile_seg, seg_tiles, st);
 }
 
 }  // namespace
@@ -476,11 +438,11 @@ bool rows_supported(int dim, int cand_count_max, bool t3, int rl, bool norm) {
 int launch_rows_screen(const AssignParams& p, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles, int64_t cap,
                        hipStream_t st) {
   const int shape = rows_shape();
-  const int R = shape == 88 ? 256 : 128;
+  const int R = shape == 883 ? 256 : 128;
   launch_tiling(p, R, tile_seg, seg_tiles, cap, st);
-  const bool ok = shape == 88   ? launch_rows_w<8, 8>(p, rl, norm, tile_seg, seg_tiles, st)
-                  : shape == 44 ? launch_rows_w<4, 4>(p, rl, norm, tile_seg, seg_tiles, st)
-                                : launch_rows_w<4, 8>(p, rl, norm, tile_seg, seg_tiles, st);
+  const bool ok = shape == 883   ? launch_rows_w<8, 8, 3>(p, rl, norm, tile_seg, seg_tiles, st)
+                  : shape == 482 ? launch_rows_w<4, 8, 2>(p, rl, norm, tile_seg, seg_tiles, st)
+                                 : launch_rows_w<4, 4, 3>(p, rl, norm, tile_seg, seg_tiles, st);
   return ok ? RQSID_OK : fail(RQSID_E_LAUNCH, "assign: row-resident screen launch failed (device query / LDS attribute)");
 }
 

@@ -397,9 +397,9 @@ STREAMED = {"default": {"RQSID_SCREEN_VARIANT": 0},
             "pp88": {"RQSID_SCREEN_VARIANT": 5, "RQSID_STREAM_SHAPE": 88},
             "res": {"RQSID_SCREEN_VARIANT": 6},  # the centre-resident screen wherever it applies
             # the row-resident screen (assign_rows.hip) wherever it applies (1-term levels: L0 and L2 here)
-            "rows44": {"RQSID_SCREEN_VARIANT": 8, "RQSID_ROWS_SHAPE": 44},
-            "rows48": {"RQSID_SCREEN_VARIANT": 8, "RQSID_ROWS_SHAPE": 48},
-            "rows88": {"RQSID_SCREEN_VARIANT": 8, "RQSID_ROWS_SHAPE": 88}}
+            "rows443": {"RQSID_SCREEN_VARIANT": 8, "RQSID_ROWS_SHAPE": 443},
+            "rows482": {"RQSID_SCREEN_VARIANT": 8, "RQSID_ROWS_SHAPE": 482},
+            "rows883": {"RQSID_SCREEN_VARIANT": 8, "RQSID_ROWS_SHAPE": 883}}
 
 
 @pytest.mark.parametrize("form", list(STREAMED))
@@ -432,7 +432,7 @@ def test_stream_kernel_equals_tile_kernel(shape, sem_name, form):
     assert (a[sel] == ref).all()
 
 
-@pytest.mark.parametrize("form", ["default", "s83", "pp88", "res", "rows48", "rows88"])
+@pytest.mark.parametrize("form", ["default", "s83", "pp88", "res", "rows443", "rows883"])
 @pytest.mark.parametrize("k", [100, 128, 200, 256])
 def test_stream_nearest_partial_tiles(k, form):
     """Single-segment nearest with k < NT*32 candidates (padding lanes masked) on the streamed path."""
@@ -500,7 +500,7 @@ def test_candidate_split_nearest(k, terms):
     assert (got == multi).all(), f"{int((got != multi).sum())} rows differ from the multi-pass screen"
     assert (got[:64] == 3).all()
     if terms == 1:  # the row-resident screen (candidate blocks with a running bound) on the same input
-        for form in ("rows48", "rows88"):
+        for form in ("rows443", "rows883"):
             rows = _with_env(STREAMED[form], lambda: ops.nearest(gpu(x), pc, screen_terms=terms).cpu().numpy())
             assert (rows == got).all(), f"{form}: {int((rows != got).sum())} rows differ"
     sel = np.arange(0, 20000, 13)
@@ -520,7 +520,7 @@ def test_candidate_split_xl_levels_equal_multi_pass():
     a = enc.encode(x).cpu().numpy()
     b = _with_env(MULTI_PASS, lambda: enc.encode(x).cpu().numpy())
     assert (a == b).all(), f"{int((a != b).any(1).sum())} rows differ between the split and multi-pass screens"
-    for form in ("rows48", "rows88"):  # the row-resident screen at the 512-candidate last level
+    for form in ("rows443", "rows883"):  # the row-resident screen at the 512-candidate last level
         c = _with_env(STREAMED[form], lambda: enc.encode(x).cpu().numpy())
         assert (c == a).all(), f"{form}: {int((c != a).any(1).sum())} rows differ"
     sel = np.arange(0, 120000, 97)
