@@ -1402,7 +1402,7 @@ int rqsid_prepare_centers(const float* centers, int64_t k, int32_t dim, uint16_t
   if (k == 0) return RQSID_OK;
   hipStream_t st = (hipStream_t)stream;
   float* scale = c_meta + 4 * k;  // row k of meta
-  if (hipMemsetAsync(scale, 0, 4 * sizeof(float), st) != hipSuccess)
+  if (fill_async(scale, 0, 4 * sizeof(float), st) != hipSuccess)
     return fail(RQSID_E_LAUNCH, "prepare_centers: hipMemsetAsync failed");
   const int64_t n = k * dim;
   const unsigned g = (unsigned)(cdiv(n, 256 * 16) < 2048 ? cdiv(n, 256 * 16) : 2048);
@@ -1478,7 +1478,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   p.den_in = den_in;
   p.den_out = den_out;
   const bool norm = res_normalize != 0;
-  if (hipMemsetAsync(workspace, 0, 256, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "assign: memset");
+  if (fill_async(workspace, 0, 256, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "assign: memset");
   const unsigned grid = (unsigned)((max_tiles + 7) / 8 * 8);  // XCD remap needs a multiple of 8
   // Measured on MI355X (tools/screen_sweep.py): independent blocks per CU beat ring depth: NT4 with
   // S=2 runs 3 blocks/CU, NT8 with S=2 runs 2 blocks/CU (RQSID_SCREEN_VARIANT=1/3 select the older

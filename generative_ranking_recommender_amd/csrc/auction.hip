@@ -221,7 +221,7 @@ int rqsid_auction_lap_full(const float* scores_wj, int32_t n_workers, int64_t n_
     // (:182-183) hands every job to worker 0 in round 1002.  The result is known without the rounds.
     if (max_rounds > 0 && max_rounds < 1002)
       return fail(RQSID_E_LAUNCH, "auction_full: no complete assignment after %d rounds", max_rounds);
-    if (hipMemsetAsync(out_assign, 0, (size_t)n_jobs * 4, st) != hipSuccess)
+    if (fill_async(out_assign, 0, (size_t)n_jobs * 4, st) != hipSuccess)
       return fail(RQSID_E_LAUNCH, "auction_full: memset");
     if (out_rounds) *out_rounds = 1002;
     return RQSID_OK;
@@ -269,7 +269,7 @@ int rqsid_auction_lap_full(const float* scores_wj, int32_t n_workers, int64_t n_
   for (int round = 0;; ++round) {
     if (max_rounds > 0 && round >= max_rounds)
       return fail(RQSID_E_LAUNCH, "auction_full: no complete assignment after %d rounds", max_rounds);
-    if (hipMemsetAsync(a.have, 0, 4, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "auction_full: memset");
+    if (fill_async(a.have, 0, 4, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "auction_full: memset");
     hipLaunchKernelGGL(full_bid_kernel, dim3((unsigned)n_workers), dim3(1024), 0, st, a, round, eps);
     hipLaunchKernelGGL(full_resolve_kernel, dim3(gj), dim3(256), 0, st, a, out_assign);
     if ((rc = check_launch("auction_full_round"))) return rc;

@@ -1591,7 +1591,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     return fail(RQSID_E_LAUNCH, "seg_auction: pinned readback buffer");
   }
   int rc = RQSID_OK;
-  if (hipMemsetAsync(a.live_count, 0, 16, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "seg_auction: memset");
+  if (fill_async(a.live_count, 0, 16, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   hipLaunchKernelGGL(sa_seg_init_kernel, dim3(gs), dim3(256), 0, st, a, active);
   hipLaunchKernelGGL(sa_multi_index_kernel, dim3(1), dim3(1024), 0, st, a);
   if ((rc = check_launch("seg_auction_init")) ||
@@ -1608,13 +1608,13 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   }
   const bool any_single = n_multi < n_seg;
   const size_t mk = (size_t)n_multi * n_workers;
-  if (n_multi > 0 && (hipMemsetAsync(a.hist, 0, mk * 256 * 4, st) != hipSuccess ||
-                      hipMemsetAsync(a.above, 0, mk * kAbovePad * 4, st) != hipSuccess ||
-                      hipMemsetAsync(a.miss, 1, mk, st) != hipSuccess ||
-                      hipMemsetAsync(a.any_miss, 0, 4, st) != hipSuccess))
+  if (n_multi > 0 && (fill_async(a.hist, 0, mk * 256 * 4, st) != hipSuccess ||
+                      fill_async(a.above, 0, mk * kAbovePad * 4, st) != hipSuccess ||
+                      fill_async(a.miss, 1, mk, st) != hipSuccess ||
+                      fill_async(a.any_miss, 0, 4, st) != hipSuccess))
     return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   // thresholds start at key 0 (a window of NaN keys: every worker takes the exact passes in round 0)
-  if (hipMemsetAsync(a.sel, 0, (size_t)n_seg * n_workers * 16, st) != hipSuccess)
+  if (fill_async(a.sel, 0, (size_t)n_seg * n_workers * 16, st) != hipSuccess)
     return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   hipLaunchKernelGGL(sa_job_init_kernel, dim3(grid_cap(cdiv(n_jobs, 256), 8192)), dim3(256), 0, st, a, n_jobs);
   const dim3 gcw((unsigned)total_chunks, (unsigned)cdiv(n_workers, kKG));
@@ -1633,8 +1633,8 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   // in most rounds); a lean block runs from a snapshot of the round state and is replayed with the full
   // rounds when any worker missed in it, so the result is the full rounds' in every case
   if (a.lst) {
-    if (hipMemsetAsync(a.lcnt, 0, (size_t)n_multi * n_workers * kAbovePad * 4, st) != hipSuccess ||
-        hipMemsetAsync(a.lbad, 1, (size_t)n_multi * n_workers, st) != hipSuccess)
+    if (fill_async(a.lcnt, 0, (size_t)n_multi * n_workers * kAbovePad * 4, st) != hipSuccess ||
+        fill_async(a.lbad, 1, (size_t)n_multi * n_workers, st) != hipSuccess)
       return fail(RQSID_E_LAUNCH, "seg_auction: memset");
     hipLaunchKernelGGL(sa_list_layout_kernel, dim3(1), dim3(1), 0, st, a);
   }
@@ -1685,14 +1685,14 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   hipGraphExec_t exec = capture(false);
   hipGraphExec_t exec_lean = n_multi > 0 && exec ? capture(true) : nullptr;
   const unsigned gsnap = (unsigned)grid_cap(cdiv(std::max<int64_t>(n_jobs, (int64_t)n_seg * n_workers * 4), 256), 4096);
-  if (hipMemsetAsync(a.live_count, 0, 4, st) != hipSuccess) rc = fail(RQSID_E_LAUNCH, "seg_auction: memset");
+  if (fill_async(a.live_count, 0, 4, st) != hipSuccess) rc = fail(RQSID_E_LAUNCH, "seg_auction: memset");
   bool try_lean = false;  // round 0 misses everywhere (thresholds start at key 0)
   for (int done = 0; rc == RQSID_OK && (max_rounds <= 0 || done < max_rounds);) {
     const int n = max_rounds > 0 ? std::min(kPoll, max_rounds - done) : kPoll;
     const bool lean = try_lean && exec_lean && n == kPoll;
     if (lean) {
       hipLaunchKernelGGL(sa_snapshot_kernel, dim3(gsnap), dim3(256), 0, st, a, out_assign, n_jobs, 0);
-      if (hipMemsetAsync(a.live_count + 2, 0, 4, st) != hipSuccess || hipGraphLaunch(exec_lean, st) != hipSuccess) {
+      if (fill_async(a.live_count + 2, 0, 4, st) != hipSuccess || hipGraphLaunch(exec_lean, st) != hipSuccess) {
         rc = fail(RQSID_E_LAUNCH, "seg_auction: graph launch");
         break;
       }
@@ -1706,7 +1706,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     }
     if ((rc = check_launch("seg_auction_round"))) break;
     if (hipMemcpyAsync(host, a.live_count, 12, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemsetAsync(a.live_count, 0, 4, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+        fill_async(a.live_count, 0, 4, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
       rc = fail(RQSID_E_LAUNCH, "seg_auction: readback");
       break;
     }
@@ -1719,7 +1719,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
       }
       if ((rc = check_launch("seg_auction_replay"))) break;
       if (hipMemcpyAsync(host, a.live_count, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-          hipMemsetAsync(a.live_count, 0, 4, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+          fill_async(a.live_count, 0, 4, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
         rc = fail(RQSID_E_LAUNCH, "seg_auction: readback");
         break;
       }
@@ -1824,7 +1824,7 @@ int rqsid_dauction_begin(const uint16_t* scores, int32_t n_workers, int64_t n_lo
                      (int32_t)n_local, (int32_t)a.total_chunks);
   hipLaunchKernelGGL(sa_seg_init_kernel, dim3(1), dim3(256), 0, st, a, (const uint8_t*)nullptr);
   hipLaunchKernelGGL(sa_multi_index_kernel, dim3(1), dim3(1024), 0, st, a);
-  if (hipMemsetAsync(a.hist, 0, (size_t)n_workers * 256 * 4, st) != hipSuccess)
+  if (fill_async(a.hist, 0, (size_t)n_workers * 256 * 4, st) != hipSuccess)
     return fail(RQSID_E_LAUNCH, "dauction: memset");
   if (n_local > 0) {
     hipLaunchKernelGGL(sa_job_init_kernel, dim3(grid_cap(cdiv(n_local, 256), 8192)), dim3(256), 0, st, a, n_local);
@@ -1882,7 +1882,7 @@ int rqsid_dauction_eqcount(const uint16_t* scores, int32_t n_workers, int64_t n_
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   if (n_local == 0) {
-    if (hipMemsetAsync(a.eqtot, 0, (size_t)n_workers * 4, st) != hipSuccess)
+    if (fill_async(a.eqtot, 0, (size_t)n_workers * 4, st) != hipSuccess)
       return fail(RQSID_E_LAUNCH, "dauction: memset");
     return RQSID_OK;
   }

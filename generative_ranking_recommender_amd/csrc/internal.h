@@ -11,6 +11,9 @@ namespace rqsid {
 // error text of the calling thread (rqsid_last_error) + status helpers
 int fail(int code, const char* fmt, ...);
 int check_launch(const char* what);
+// hipMemsetAsync's job done by a kernel (the default): inside a captured HIP graph a kernel node is ordered
+// like every other kernel of the stream.  RQSID_MEMSET_API=1 uses hipMemsetAsync (A/B, graph diagnosis).
+hipError_t fill_async(void* p, int value, size_t bytes, hipStream_t st);
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

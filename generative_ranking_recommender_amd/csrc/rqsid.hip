@@ -31,6 +31,34 @@ int check_launch(const char* what) {
 }
 
 namespace {
+__global__ __launch_bounds__(256) void fill_words_kernel(uint32_t* __restrict__ p, int64_t n, uint32_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = v;
+}
+__global__ __launch_bounds__(256) void fill_bytes_kernel(uint8_t* __restrict__ p, int64_t n, uint8_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = v;
+}
+}  // namespace
+
+hipError_t fill_async(void* p, int value, size_t bytes, hipStream_t st) {
+  static const bool api = [] {
+    const char* e = getenv("RQSID_MEMSET_API");
+    return e && atoi(e) != 0;
+  }();
+  if (api) return hipMemsetAsync(p, value, bytes, st);
+  if (bytes == 0) return hipSuccess;
+  const uint8_t b = (uint8_t)value;
+  if (((uintptr_t)p & 3) == 0 && (bytes & 3) == 0) {
+    const int64_t n = (int64_t)(bytes / 4);
+    hipLaunchKernelGGL(fill_words_kernel, dim3(grid_cap(cdiv(n, 256), 1024)), dim3(256), 0, st, (uint32_t*)p, n,
+                       0x01010101u * b);
+  } else {
+    const int64_t n = (int64_t)bytes;
+    hipLaunchKernelGGL(fill_bytes_kernel, dim3(grid_cap(cdiv(n, 256), 1024)), dim3(256), 0, st, (uint8_t*)p, n, b);
+  }
+  return hipGetLastError();
+}
+
+namespace {
 constexpr int kAccTileRows = 256;  // rows per centroid-accumulate tile
 constexpr int kBucketLdsBins = 16384;
 }  // namespace
@@ -556,7 +584,7 @@ int rqsid_bucket(const int32_t* keys, int64_t n, int32_t S, int32_t tile_rows, i
   hipStream_t st = (hipStream_t)stream;
   int32_t* counts = (int32_t*)workspace;
   int32_t* cursor = counts + S;
-  if (hipMemsetAsync(counts, 0, (size_t)S * 4, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "bucket: memset");
+  if (fill_async(counts, 0, (size_t)S * 4, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "bucket: memset");
   const size_t lds = S <= kBucketLdsBins ? (size_t)S * 4 : 0;
   if (n > 0) {
     hipLaunchKernelGGL(bucket_hist_kernel, dim3(grid_cap(cdiv(n, 256 * 16), 2048)), dim3(256), lds, st, keys, n,
