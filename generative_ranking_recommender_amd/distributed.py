@@ -392,5 +392,10 @@ def sharded_balanced_assign(x_local: torch.Tensor, centers: torch.Tensor, n_glob
     """auction_lap_half(-pairwise_distance(X, C)) with X row-sharded: each rank scores its rows against all
     centres (rqsid_auction_scores) and the ranks run one ShardedAuction.  Returns this rank's worker ids."""
     w = ops.auction_scores(x_local.contiguous(), centers.float().contiguous(), half=half)
+    if dist.get_world_size(group) == 1:
+        # one rank holds every job: the single-process auction of the same scores (identical assignment,
+        # see ShardedAuction), which also runs the bid-list rounds the per-round collectives cannot
+        a, _ = ops.auction(w)
+        return a.long()
     a, _ = ShardedAuction(group).run(GpuAuctionPasses(w, n_global), n_global, centers.shape[0])
     return a.long()

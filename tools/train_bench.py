@@ -1,7 +1,9 @@
-"""Time HierarchicalRQKMeans.train at the PROD shape (layer_clusters [128,1280,1280], need [128,128,256])
-on synthetic rows, per layer, with the lockstep sub-fits (default) or the reference's sequential order.
+"""Time HierarchicalRQKMeans.train at the PROD shape (layer_clusters [128,1280,1280], need [128,128,256]) or
+the XL shape (configs[4]: [256,2560,2560], need [256,256,512]) on synthetic rows, per layer, with the
+lockstep sub-fits (default) or the reference's sequential order; --sharded runs the row-sharded trainer
+(one process per GPU) at world size 1 over RCCL, i.e. the code path of one rank of the 8-GPU job.
 
-    python tools/train_bench.py --rows 200000 [--sequential] [--out gpurun_out/train.json]
+    python tools/train_bench.py --rows 200000 [--sequential] [--preset xl] [--sharded] [--out f.json]
 
 Prints one JSON line: rows, per-layer seconds, total seconds, sub-fit mode."""
 import argparse
@@ -39,6 +41,9 @@ def main():
     ap.add_argument("--rows", type=int, default=200000)
     ap.add_argument("--sequential", action="store_true")
     ap.add_argument("--iter-limit", type=int, default=100)
+    ap.add_argument("--preset", choices=("prod", "xl"), default="prod")
+    ap.add_argument("--sharded", action="store_true",
+                    help="row-sharded trainer through a world-size-1 RCCL process group")
     ap.add_argument("--out", default="")
     ap.add_argument("--data", choices=("small", "bench"), default="small",
                     help="small: synth.small_mixture (host); bench: bench.make_rows (the encode bench's rows, "
@@ -57,15 +62,24 @@ def main():
         x = bench.make_rows(a.rows, 0, torch.device("cuda", 0)).cpu().numpy()
     else:
         x = synth.small_mixture(a.rows, m=4096, seed=5)
-    cfg = HierarchicalRQKMeansConfig(layer_clusters=[128, 1280, 1280], need_clusters=[128, 128, 256],
-                                     embedding_dim=512, iter_limit=a.iter_limit)
+    lc, need = ([256, 2560, 2560], [256, 256, 512]) if a.preset == "xl" else ([128, 1280, 1280], [128, 128, 256])
+    cfg = HierarchicalRQKMeansConfig(layer_clusters=lc, need_clusters=need, embedding_dim=512,
+                                     iter_limit=a.iter_limit)
+    group = None
+    if a.sharded:
+        import os
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        group = dist.group.WORLD
     h = LayerTimes()
     lg = logging.getLogger("generative_ranking_recommender_amd.hierarchical_rq_kmeans")
     lg.setLevel(logging.INFO)
     lg.addHandler(h)
     np.random.seed(42)
     torch.manual_seed(42)
-    model = HierarchicalRQKMeans(cfg, device=torch.device("cuda", 0))
+    model = HierarchicalRQKMeans(cfg, device=torch.device("cuda", 0), group=group)
     model.batched_sub_fits = not a.sequential
     t = time.time()
     res = model.train(x)
@@ -73,7 +87,9 @@ def main():
     total = time.time() - t
     ids = np.stack([r.cpu().numpy() for r in res["cluster_ids"]], 1)
     consistent = bool((model.predict(x, reference_quirks=False) == ids).all())
-    line = {"rows": a.rows, "data": a.data, "mode": "sequential" if a.sequential else "lockstep",
+    line = {"rows": a.rows, "data": a.data, "preset": a.preset, "layer_clusters": lc, "need_clusters": need,
+            "path": "sharded (world 1, RCCL)" if a.sharded else "single process",
+            "mode": "sequential" if a.sequential else "lockstep",
             "total_s": round(total, 2),
             "layers": [m for m in h.marks], "unique_ids": int(len(np.unique(ids, axis=0))),
             "train_encode_consistent": consistent}
