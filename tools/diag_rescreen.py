@@ -60,6 +60,21 @@ def main():
         else:
             x, gen = r2_rows(n, dev)
             c = x[torch.randperm(n, device=dev, generator=gen)[:k]].clone()
+        if kind == "r2":
+            # what the overflowing rows look like: NaN / zero rows and centres, and the fp64 distance
+            # spread of a few rows' nearest candidates
+            xs = x[:64].double()
+            d = torch.cdist(xs, c.double()) ** 2
+            srt = torch.sort(d, dim=1).values
+            print(json.dumps({"input": kind, "nan_rows": int(torch.isnan(x).any(1).sum()),
+                              "nan_centres": int(torch.isnan(c).any(1).sum()),
+                              "zero_rows": int((x.abs().sum(1) == 0).sum()),
+                              "zero_centres": int((c.abs().sum(1) == 0).sum()),
+                              "row_norm_min_max": [float(x.norm(dim=1).min()), float(x.norm(dim=1).max())],
+                              "unique_centres": int(torch.unique(c, dim=0).shape[0]),
+                              "d2_best9_of_row0": [float(v) for v in srt[0, :9]],
+                              "within_1e-4_of_min": [int(v) for v in ((srt - srt[:, :1]) <= 1e-4).sum(1)[:16]]}),
+                  flush=True)
         pc = ops.prepare_centers(c)
         ws = ops.AssignWorkspace(n, dev)
         for nr in ("0", "1"):
