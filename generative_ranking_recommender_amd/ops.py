@@ -46,12 +46,16 @@ def centroid_tile_rows() -> int:
     return int(lib().rqsid_centroid_tile_rows())
 
 
+kMaxList = 8  # candidates a screen can list per row (assign_common.h)
+
+
 @dataclass
 class PreparedCenters:
     """Centres + the derived data rqsid_assign reads (fp16 copy and screening-bound norms)."""
     centers: torch.Tensor      # f32 [K, D]
     c16: torch.Tensor          # int16 [K, D/32, 2, 32]: per 32-dim chunk the hi then lo fp16 terms of c 2^s
     meta: torch.Tensor         # f32 [K+1, 4]: |c|^2, |c|, |2-term residual|, |1-term residual|; row K: 2^-s
+    nearest_cand: Optional["Candidates"] = None  # nearest()'s candidate list (duplicates dropped), built once
 
     @property
     def k(self) -> int:
@@ -246,9 +250,14 @@ def nearest(x: torch.Tensor, pc: PreparedCenters, workspace: Optional[AssignWork
     """Unconstrained nearest centre (KMeans.predict / pairwise_distance_full + argmin)."""
     n = x.shape[0]
     b = single_segment(n, x.device)
-    cand = Candidates(torch.zeros(1, dtype=torch.int32, device=x.device),
-                      torch.full((1,), pc.k, dtype=torch.int32, device=x.device), pc.k)
-    return assign(x, pc, b, cand, workspace=workspace, screen_terms=screen_terms)[1]
+    if pc.nearest_cand is None:
+        cand = Candidates(torch.zeros(1, dtype=torch.int32, device=x.device),
+                          torch.full((1,), pc.k, dtype=torch.int32, device=x.device), pc.k)
+        # bitwise-duplicate centres (e.g. several K-Means centres initialised from equal rows): only the
+        # first copy can be the argmin, and with the copies in the list every row nearest to them is an
+        # exact > 8-way tie that no screen can split, i.e. an all-candidate fp64 re-score
+        pc.nearest_cand = dedup_candidates(cand, pc.centers) if pc.k > kMaxList else cand
+    return assign(x, pc, b, pc.nearest_cand, workspace=workspace, screen_terms=screen_terms)[1]
 
 
 def _groups_tensor(group_dims: Sequence[int], device) -> torch.Tensor:

@@ -580,3 +580,25 @@ def test_rescreen_of_overflowing_rows_keeps_exact_ids(k, dups, monkeypatch):
     assert np.array_equal(out["0"][smp], exact_ids(x[smp], c))
     if dups:
         assert (out["0"][:500] == 7).all()
+
+def test_nearest_with_many_duplicate_centres():
+    """K-Means centres initialised from rows that are exactly equal (here: zero rows, as a normalised
+    residual of a one-member cluster is) make every row nearest to them an exact many-way tie.  nearest()
+    drops the later copies (only the first can be the argmin), so the screen lists those rows instead of
+    re-scoring all K candidates; the IDs equal the exact oracle's, ties to the lowest index."""
+    rng = np.random.default_rng(77)
+    k, n = 2560, 20000
+    c = rng.standard_normal((k, 512)).astype(np.float32)
+    c /= np.linalg.norm(c, axis=1, keepdims=True)
+    dup = rng.choice(k, 300, replace=False)
+    c[dup] = 0.0                       # 300 identical (zero) centres
+    x = rng.standard_normal((n, 512)).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    x[:500] = 0.0                      # rows on the duplicated centre
+    pc = ops.prepare_centers(gpu(c))
+    ws = ops.AssignWorkspace(n, DEV)
+    got = ops.nearest(gpu(x), pc, workspace=ws).cpu().numpy()
+    assert pc.nearest_cand.count_max == k - 299
+    assert (got[:500] == dup.min()).all()
+    sel = np.arange(0, n, 7)
+    assert (got[sel] == exact_ids(x[sel], c)).all()
