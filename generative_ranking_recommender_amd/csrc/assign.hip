@@ -908,19 +908,27 @@ __device__ __forceinline__ double half_sum(double v) {
   return v;
 }
 
+// mode 0: every work item; after the fp32 re-screen the items it left "every candidate" (n = -1: a true
+// cluster of > kMaxList candidates, e.g. near-equal distances of a zero residual row) go to their own pass
+// instead: mode 1 takes the other items, mode 2 the n = -1 items in overflow-list order, where a block's 8
+// consecutive items are rows of one segment walking the same candidates, so a candidate row is read from
+// L2 once per block rather than once per row (the per-row arithmetic is the same code)
+constexpr int kOvfSlot = 56;  // workspace header int: overflow item count
 template <int RL, bool NORM>
-__global__ __launch_bounds__(256) void assign_rescore_half_kernel(AssignParams p) {
+__global__ __launch_bounds__(256) void assign_rescore_half_kernel(AssignParams p, const int32_t* __restrict__ ovf_list,
+                                                                  int mode) {
   constexpr int kV = kHalfDim / 128;  // float4 per lane
   const int lane = threadIdx.x & 63, hl = lane & 31, hh = lane >> 5;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int nw = gridDim.x * 4;
-  const int64_t nitems_raw = *p.work_count;
+  const int64_t nitems_raw = mode == 2 ? p.work_count[kOvfSlot] : *p.work_count;
   const int64_t nitems = nitems_raw < p.work_cap ? nitems_raw : p.work_cap;
   const int nv = p.dim / 4;
   for (int64_t it0 = 2 * (int64_t)wid; it0 < nitems; it0 += 2 * (int64_t)nw) {
-    const bool active = it0 + hh < nitems;  // an idle half repeats its partner's item and writes nothing
-    const int64_t it = active ? it0 + hh : it0;
-    const WorkItem w = p.work[p.work_idx ? p.work_idx[it] : it];
+    const int64_t it = it0 + hh < nitems ? it0 + hh : it0;
+    const WorkItem w = p.work[mode == 2 ? ovf_list[it] : (p.work_idx ? p.work_idx[it] : it)];
+    // an idle half (past the end, or an item of the other pass) repeats the work and writes nothing
+    const bool active = it0 + hh < nitems && (mode == 0 || (mode == 1 ? w.n != -1 : w.n == -1));
     const float* xr = p.x + (int64_t)w.row * p.dim;
     const float* car = RL >= 1 ? p.ca + (int64_t)seg_row(p.seg_ca, w.seg) * p.dim : nullptr;
     const float* cbr = RL >= 2 ? p.cb + (int64_t)seg_row(p.seg_cb, w.seg) * p.dim : nullptr;
@@ -962,7 +970,7 @@ __global__ __launch_bounds__(256) void assign_rescore_half_kernel(AssignParams p
     const bool penalty = w.n == -2;
     const bool listed = w.n >= 1;
     const int base = p.cand_base[w.seg];
-    const int n = listed ? w.n : (penalty ? p.n_centers : (w.n == -1 ? p.cand_count[w.seg] : 0));
+    const int n = !active ? 0 : listed ? w.n : (penalty ? p.n_centers : (w.n == -1 ? p.cand_count[w.seg] : 0));
     const int nmax = max(n, __shfl_xor(n, 32));  // both halves run the same batches
     double best = INFINITY;
     int bj = INT_MAX;
@@ -1061,8 +1069,6 @@ __global__ __launch_bounds__(256) void assign_rescore_half_kernel(AssignParams p
 // the list; it contains every candidate the fp64 argmin can return, so IDs are unchanged.
 // Block layout: 8 half-waves take 8 consecutive overflow items and walk the candidates together, so
 // rows of one segment read each candidate row from L1 / L2 once per block, not once per row.
-constexpr int kOvfSlot = 56;  // workspace header int: overflow item count
-
 __global__ __launch_bounds__(256) void overflow_list_kernel(AssignParams p, int32_t* __restrict__ ovf_list) {
   const int64_t nitems_raw = *p.work_count;
   const int64_t nitems = nitems_raw < p.work_cap ? nitems_raw : p.work_cap;
@@ -1569,9 +1575,10 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   const bool half = dim <= kHalfDim && !(ef && atoi(ef));
   // rows the screen left with "every candidate" get an fp32 list first (RQSID_NO_RESCREEN=1: off, A/B)
   const char* nr = getenv("RQSID_NO_RESCREEN");
+  int32_t* ovf_list = nullptr;
   if (dim <= kHalfDim && !(nr && atoi(nr)) && cand_count_max > kMaxList) {
-    int32_t* ovf_list = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(work_idx) + (n_rows * 4 + 255) / 256 * 256 +
-                                                   resident_desc_bytes(n_rows));
+    ovf_list = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(work_idx) + (n_rows * 4 + 255) / 256 * 256 +
+                                          resident_desc_bytes(n_rows));
     hipLaunchKernelGGL(overflow_list_kernel, dim3(grid_cap(cdiv(n_rows, 256), 1024)), dim3(256), 0, st, p, ovf_list);
 #define RQ_RSC(RL, NORM) hipLaunchKernelGGL((assign_rescreen_kernel<RL, NORM>), dim3(2048), dim3(256), 0, st, p, ovf_list)
     if (res_levels == 0) RQ_RSC(0, false);
@@ -1582,10 +1589,16 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
 #undef RQ_RSC
     if ((rc = check_launch("assign_rescreen"))) return rc;
   }
-#define RQ_RS(RL, NORM)                                                                          \
-  do {                                                                                           \
-    if (half) hipLaunchKernelGGL((assign_rescore_half_kernel<RL, NORM>), g, dim3(256), 0, st, p); \
-    else hipLaunchKernelGGL((assign_rescore_kernel<RL, NORM>), g, dim3(256), 0, st, p);           \
+#define RQ_RS(RL, NORM)                                                                                       \
+  do {                                                                                                        \
+    if (half && ovf_list) {                                                                                   \
+      hipLaunchKernelGGL((assign_rescore_half_kernel<RL, NORM>), g, dim3(256), 0, st, p, ovf_list, 1);          \
+      hipLaunchKernelGGL((assign_rescore_half_kernel<RL, NORM>), g, dim3(256), 0, st, p, ovf_list, 2);          \
+    } else if (half) {                                                                                        \
+      hipLaunchKernelGGL((assign_rescore_half_kernel<RL, NORM>), g, dim3(256), 0, st, p, (const int32_t*)nullptr, 0); \
+    } else {                                                                                                  \
+      hipLaunchKernelGGL((assign_rescore_kernel<RL, NORM>), g, dim3(256), 0, st, p);                          \
+    }                                                                                                         \
   } while (0)
   if (res_levels == 0) RQ_RS(0, false);
   else if (res_levels == 1 && norm) RQ_RS(1, true);
