@@ -93,11 +93,11 @@ LEVEL_KERNELS = {
     "prod": {0: ("assign_screen_kernel<4, 2, 0, false, false, true, 1>", "assign_rescore_half_kernel<0, false>"),
              1: ("assign_screen_kernel<4, 2, 1, true, true, true, 1>", "assign_rescore_half_kernel<1, true>"),
              2: ("assign_pp_kernel<8, 2, true, false>", "assign_rescore_half_kernel<2, true>")},
-    # [256,256,512]: 256-candidate level 0 (per-tile form); 256-candidate 3-term level 1 and 512-candidate
-    # level 2 in one pass each (candidate-split screen, CW = 2)
+    # [256,256,512]: 256-candidate level 0 (per-tile form); 256-candidate 3-term level 1 in one pass
+    # (candidate-split screen, CW = 2); 512-candidate level 2 on the row-resident screen (assign_rows.hip)
     "xl": {0: ("assign_screen_kernel<8, 2, 0, false, false, true, 1>", "assign_rescore_half_kernel<0, false>"),
            1: ("assign_screen_kernel<4, 2, 1, true, true, true, 2>", "assign_rescore_half_kernel<1, true>"),
-           2: ("assign_screen_kernel<8, 2, 2, true, false, true, 2>", "assign_rescore_half_kernel<2, true>")}}
+           2: ("assign_rows_kernel<4, 4, 3, 2, 2, true>", "assign_rescore_half_kernel<2, true>")}}
 PRESET = "prod"
 
 

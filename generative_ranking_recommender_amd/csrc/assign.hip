@@ -1523,8 +1523,11 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   const bool use_res = res_ok && variant == 6;
   // the row-resident screen (assign_rows.hip): variant 8 forces it wherever it applies (1-term levels of
   // 512-d rows with <= 512 candidates)
-  const bool use_rows = variant == 8 && rows_supported(dim, cand_count_max, t3, res_levels, norm) &&
-                        (int64_t)n_segments + 1 <= n_rows;
+  // default for 1-term residual levels wider than 256 candidates (the XL preset's 512-candidate last level:
+  // 7.0 vs 14.8 ms for the candidate-split screen, profiles/r4_xl_rows_ab.txt); the 256-candidate PROD level
+  // keeps the ping-pong form (7.4 vs 7.6-7.8 ms)
+  const bool use_rows = (variant == 8 || (variant == 0 && res_levels >= 1 && cand_count_max > 256)) &&
+                        rows_supported(dim, cand_count_max, t3, res_levels, norm) && (int64_t)n_segments + 1 <= n_rows;
   if (use_rows) {
     // R-row tile offsets in the compact-list area, the tile map in the tile_seg slot; compact work list
     if ((rc = launch_rows_screen(p, res_levels, norm, tile_seg, work_idx, n_rows, st))) return rc;

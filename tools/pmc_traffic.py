@@ -34,10 +34,13 @@ def main(root, rows):
     for k, cs in vals.items():
         fetch = cs.get("FETCH_SIZE", [])
         write = cs.get("WRITE_SIZE", [])
-        # the last launch of each kernel is a timed-step launch (warm-up and count passes come first)
-        out[k] = {"launches": max(len(fetch), len(write)),
-                  "fetch_bytes": 2 * 1024 * fetch[-1] if fetch else None,
-                  "write_bytes": 1024 * write[-1] if write else None}
+        # the last launch of each kernel is a timed-step launch (warm-up and count passes come first); the
+        # re-score runs as two launches per level after the fp32 re-screen (listed rows, then the overflow
+        # pass): its level bytes are the last two launches
+        last = 2 if "assign_rescore_half_kernel" in k else 1
+        out[k] = {"launches": max(len(fetch), len(write)), "launches_per_level": last,
+                  "fetch_bytes": 2 * 1024 * sum(fetch[-last:]) if fetch else None,
+                  "write_bytes": 1024 * sum(write[-last:]) if write else None}
         if fetch and write:
             out[k]["hbm_bytes"] = out[k]["fetch_bytes"] + out[k]["write_bytes"]
     print(json.dumps({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), FETCH_SIZE x2 (gfx950)",
