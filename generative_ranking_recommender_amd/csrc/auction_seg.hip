@@ -104,6 +104,7 @@ struct SegAuction {
   int64_t* loff;                 // [n_multi]
   int32_t* lcs;                  // [n_multi]: capacity per worker, 4 * (N_s / K) + 256
 };
+constexpr int64_t kListMaxJpw = 16384;  // lists only while the average jobs per worker per segment is at most this
 constexpr int kListDelta = 64;   // keys below last round's threshold kept in the bid list
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ off, int n_seg, int64_t i) {
@@ -1514,9 +1515,12 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.s_rounds = snap ? c.take<int32_t>(S) : nullptr;
   // the bid lists of the multi-chunk segments (RQSID_AUCTION_LIST=0: the sweep, for A/B): segment s holds
   // K * (4 * (N_s / K) + 256) <= 4 N_s + 256 K entries
+  // Only while a worker's list is short enough for its one block: at ~80k jobs per worker (K=128 over 10M
+  // rows) the one-block-per-worker list round lost to the sweep (10M PROD training, level 1: 23 -> 33 s)
   const char* el = getenv("RQSID_AUCTION_LIST");
-  const bool list = guess && a.n_multi > 0 && !(el && !atoi(el));
   const int64_t nm = a.n_multi > 0 ? a.n_multi : 1;
+  const int lmode = el ? atoi(el) : 1;  // 0: sweep only; 1: lists within kListMaxJpw (default); 2: lists always
+  const bool list = guess && a.n_multi > 0 && lmode != 0 && (lmode == 2 || N / (nm * K) <= kListMaxJpw);
   a.lst = list ? c.take<uint2>(4 * N + 256 * (int64_t)K * nm) : nullptr;
   a.lcnt = list ? c.take<uint32_t>(nm * K * kAbovePad) : nullptr;
   a.lkb = list ? c.take<uint32_t>(nm * K) : nullptr;
