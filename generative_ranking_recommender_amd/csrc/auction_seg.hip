@@ -103,8 +103,19 @@ struct SegAuction {
   uint8_t* lbad;                 // [n_multi*K]: 1 = the worker takes the sweep path this round
   int64_t* loff;                 // [n_multi]
   int32_t* lcs;                  // [n_multi]: capacity per worker, 4 * (N_s / K) + 256
+  // multi-block list rounds (one wide segment, long lists; sa_mlist_* kernels): entry chunks per worker
+  // (0: the one-block-per-worker sa_list_round_kernel), per worker the two radix histograms, {b1, above, T,
+  // need}, the jobs of the values equal to T, their count and the round's list verdict
+  int32_t lmb_chunks;
+  uint32_t* lh;                  // [n_multi*K][512]
+  uint32_t* lsel;                // [n_multi*K][4]
+  uint32_t* leq;                 // [n_multi*K][kListEq]
+  uint32_t* leqn;                // [n_multi*K]
+  uint8_t* lok;                  // [n_multi*K]
 };
-constexpr int64_t kListMaxJpw = 16384;  // lists only while the average jobs per worker per segment is at most this
+constexpr int64_t kListMaxJpw = 16384;  // one-block list rounds only while the average jobs per worker per segment is at most this
+constexpr int64_t kListBlockJpw = 4096;  // one wide segment above this many jobs per worker: multi-block list rounds
+constexpr int kMCH = 2048;               // list entries per block of a multi-block list round
 constexpr int kListDelta = 64;   // keys below last round's threshold kept in the bid list
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ off, int n_seg, int64_t i) {
@@ -1358,6 +1369,197 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
   }
 }
 
+// ---- multi-block list rounds: sa_list_round_kernel's steps for long lists (one wide segment), each a grid
+// over (worker, chunk of kMCH entries) or one block per worker, so a round of a K=128 x 10M auction is not
+// 128 blocks walking ~230k entries each.  Same values, selection, tie ranks and bids; a worker whose list
+// fails in any step (lok = 0, lbad = 1) takes the sweep path of the same round before any of its bids.
+__device__ __forceinline__ void mlist_fail(const SegAuction& a, int64_t hw) {
+  a.lok[hw] = 0;
+  a.lbad[hw] = 1;
+  a.lcnt[hw * kAbovePad] = 0;  // the sweep's guessed pass rebuilds it
+}
+
+// validity (as sa_list_round_kernel's first test) and zeroed histograms; one block per worker
+__global__ __launch_bounds__(256) void sa_mlist_init_kernel(SegAuction a) {
+  const int64_t hw = blockIdx.x;
+  const int r = (int)(hw / a.K), w = (int)(hw % a.K);
+  const int sg = a.mseg[r];
+  const int tid = threadIdx.x;
+  if (!(a.flag[sg] & kLive)) {
+    if (tid == 0) a.lok[hw] = 0;
+    return;
+  }
+  a.lh[hw * 512 + tid] = 0;
+  a.lh[hw * 512 + 256 + tid] = 0;
+  if (tid == 0) {
+    const uint32_t n = a.lcnt[hw * kAbovePad], cap = (uint32_t)a.lcs[r], kb = a.lkb[hw];
+    const int counter = *a.round_dev;
+    const int64_t sw = (int64_t)sg * a.K + w;
+    a.leqn[hw] = 0;
+    if (n == 0 || n > cap || counter > 1000 || a.sel[sw * 4 + 2] < kb) mlist_fail(a, hw);
+    else a.lok[hw] = 1;
+  }
+}
+
+// STEP 0: this round's keys (kept in the entries' upper 16 bits) and the high-byte histogram of the keys
+// >= lkb; 1: the low-byte histogram of bin b1; 2: the jobs of the values equal to T (when some of them bid);
+// 3: the bids.  Grid: workers x lmb_chunks blocks.
+template <int STEP>
+__global__ __launch_bounds__(256) void sa_mlist_pass_kernel(SegAuction a) {
+  const int64_t hw = blockIdx.x / a.lmb_chunks;
+  const uint32_t i0 = (uint32_t)(blockIdx.x % a.lmb_chunks) * kMCH;
+  if (!a.lok[hw]) return;
+  const uint32_t n = a.lcnt[hw * kAbovePad];
+  if (i0 >= n) return;
+  const uint32_t i1 = min(n, i0 + (uint32_t)kMCH);
+  const int r = (int)(hw / a.K), w = (int)(hw % a.K);
+  const int tid = threadIdx.x;
+  uint2* const L = a.lst + a.loff[r] + (int64_t)w * a.lcs[r];
+  const uint32_t kb = a.lkb[hw];
+  if (STEP == 0 || STEP == 1) {
+    __shared__ uint32_t hst[256];
+    hst[tid] = 0;
+    __syncthreads();
+    const uint32_t b1 = STEP == 1 ? a.lsel[hw * 4] : 0u;
+    for (uint32_t i = i0 + tid; i < i1; i += 256) {
+      if (STEP == 0) {
+        const uint2 e = L[i];
+        const uint32_t k = okey(value_bits(w, (uint16_t)e.y, a.hb[e.x], a.cost[e.x]));
+        L[i].y = (e.y & 0xFFFFu) | (k << 16);
+        if (k >= kb) atomicAdd(&hst[k >> 8], 1u);
+      } else {
+        const uint32_t k = L[i].y >> 16;
+        if (k >= kb && (k >> 8) == b1) atomicAdd(&hst[k & 255u], 1u);
+      }
+    }
+    __syncthreads();
+    if (hst[tid]) atomicAdd(&a.lh[hw * 512 + STEP * 256 + tid], hst[tid]);
+    return;
+  }
+  const uint32_t T = a.lsel[hw * 4 + 2], need = a.lsel[hw * 4 + 3];
+  if (STEP == 2) {
+    if (!need) return;
+    for (uint32_t i = i0 + tid; i < i1; i += 256) {
+      const uint2 e = L[i];
+      if ((e.y >> 16) == T) {
+        const uint32_t q = atomicAdd(&a.leqn[hw], 1u);
+        if (q < (uint32_t)kListEq) a.leq[hw * kListEq + q] = e.x;
+      }
+    }
+    return;
+  }
+  // STEP 3: bids, exactly as sa_list_round_kernel's last pass (leq sorted by sa_mlist_eq_kernel)
+  const int sg = a.mseg[r];
+  const uint32_t neq = min(a.leqn[hw], (uint32_t)kListEq);
+  const uint32_t* eqj = a.leq + hw * kListEq;
+  const uint16_t eps = a.eps[sg];
+  const _Float16 epsh = __builtin_bit_cast(_Float16, eps);
+  const _Float16 vT = __builtin_bit_cast(_Float16, okey_inv(T));
+  const bool ret = *a.round_dev < 100;
+  for (uint32_t i = i0 + tid; i < i1; i += 256) {
+    const uint2 e = L[i];
+    const uint32_t j = e.x, k = e.y >> 16;
+    uint32_t bid = 0;
+    if (k > T) {
+      const _Float16 x = __builtin_bit_cast(_Float16, okey_inv(k));
+      bid = __builtin_bit_cast(uint16_t, (_Float16)((_Float16)(x - vT) + epsh));
+    } else if (k == T && need) {
+      uint32_t lo = 0, hi = neq;  // rank of j among the equal values' jobs
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (eqj[mid] < j) lo = mid + 1; else hi = mid;
+      }
+      if (lo < need) bid = eps;
+    }
+    if (ret && a.hb[j] == w) bid = eps;  // retention: the previous winner bids eps on its job
+    if (bid) atomicMax(&a.key[j], (bid << 16) | (0xFFFFu - (uint32_t)w));
+  }
+}
+
+// the selections: STEP 0 the high byte b1 (>= jpw + 1 values at or above lkb, else the list fails); STEP 1
+// the low byte, T and need.  One wave per worker.
+template <int STEP>
+__global__ __launch_bounds__(64) void sa_mlist_select_kernel(SegAuction a) {
+  const int64_t hw = blockIdx.x;
+  if (!a.lok[hw]) return;
+  const int r = (int)(hw / a.K);
+  const int sg = a.mseg[r];
+  const int lane = threadIdx.x;
+  const uint32_t jpw = (uint32_t)((a.seg_off[sg + 1] - a.seg_off[sg]) / a.K);
+  const uint32_t* h = a.lh + hw * 512 + STEP * 256;
+  uint32_t* sel = a.lsel + hw * 4;
+  if (STEP == 0) {
+    uint32_t tot = h[4 * lane] + h[4 * lane + 1] + h[4 * lane + 2] + h[4 * lane + 3];
+    for (int o = 32; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o);
+    if (tot < jpw + 1) {  // fewer than jpw + 1 values at or above the list base
+      if (lane == 0) mlist_fail(a, hw);
+      return;
+    }
+    uint32_t b = 0, above = 0;
+    wave_select(h, jpw + 1, b, above);
+    if (lane == 0) {
+      sel[0] = b;
+      sel[1] = above;
+    }
+  } else {
+    uint32_t b = 0, above = 0;
+    wave_select(h, jpw + 1 - sel[1], b, above);
+    if (lane == 0) {
+      const uint32_t T = (sel[0] << 8) | b;
+      sel[2] = T;
+      sel[3] = jpw - (sel[1] + above);
+      if (T < a.lkb[hw]) mlist_fail(a, hw);  // (cannot happen with >= jpw + 1 values >= lkb; a guard)
+    }
+  }
+}
+
+// the equal values' jobs in ascending order (bitonic sort in LDS), the round's selection published and the
+// list verdict; one block per worker
+__global__ __launch_bounds__(kLT) void sa_mlist_eq_kernel(SegAuction a) {
+  const int64_t hw = blockIdx.x;
+  if (!a.lok[hw]) return;
+  const int r = (int)(hw / a.K), w = (int)(hw % a.K);
+  const int sg = a.mseg[r];
+  const int tid = threadIdx.x;
+  __shared__ uint32_t eqj[kListEq];
+  const uint32_t T = a.lsel[hw * 4 + 2], need = a.lsel[hw * 4 + 3];
+  const uint32_t neq = need ? a.leqn[hw] : 0u;
+  if (neq > (uint32_t)kListEq) {
+    if (tid == 0) mlist_fail(a, hw);
+    return;
+  }
+  uint32_t* const g = a.leq + hw * kListEq;
+  if (neq > 1) {
+    uint32_t m = 1;
+    while (m < neq) m <<= 1;
+    for (uint32_t i = tid; i < m; i += kLT) eqj[i] = i < neq ? g[i] : 0xFFFFFFFFu;
+    __syncthreads();
+    for (uint32_t kk = 2; kk <= m; kk <<= 1)
+      for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+        for (uint32_t i = tid; i < m; i += kLT) {
+          const uint32_t p = i ^ jj;
+          if (p > i) {
+            const uint32_t x = eqj[i], y = eqj[p];
+            if ((x > y) == ((i & kk) == 0)) {
+              eqj[i] = y;
+              eqj[p] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    for (uint32_t i = tid; i < neq; i += kLT) g[i] = eqj[i];
+  }
+  if (tid == 0) {
+    uint32_t* sel = a.sel + ((int64_t)sg * a.K + w) * 4;
+    sel[0] = T >> 8;
+    sel[1] = 0;
+    sel[2] = T;
+    sel[3] = need;
+    a.lbad[hw] = 0;
+  }
+}
+
 // list regions: segment r's K lists of 4 * (N_s / K) + 256 entries each, in multi-chunk segment order
 __global__ void sa_list_layout_kernel(SegAuction a) {
   int64_t off = 0;
@@ -1519,8 +1721,17 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   // rows) the one-block-per-worker list round lost to the sweep (10M PROD training, level 1: 23 -> 33 s)
   const char* el = getenv("RQSID_AUCTION_LIST");
   const int64_t nm = a.n_multi > 0 ? a.n_multi : 1;
-  const int lmode = el ? atoi(el) : 1;  // 0: sweep only; 1: lists within kListMaxJpw (default); 2: lists always
-  const bool list = guess && a.n_multi > 0 && lmode != 0 && (lmode == 2 || N / (nm * K) <= kListMaxJpw);
+  const int lmode = el ? atoi(el) : 1;  // 0: sweep only; 1: lists (default); 2: one-block lists at any size
+  // one wide segment with long lists: the multi-block list rounds (any jobs per worker); otherwise one block
+  // per worker while the lists are short
+  const bool mb = guess && a.n_multi == 1 && lmode == 1 && N / K > kListBlockJpw;
+  const bool list = guess && a.n_multi > 0 && lmode != 0 && (lmode == 2 || mb || N / (nm * K) <= kListMaxJpw);
+  a.lmb_chunks = mb ? (int32_t)((4 * (N / K) + 256 + kMCH - 1) / kMCH) : 0;
+  a.lh = mb ? c.take<uint32_t>(nm * K * 512) : nullptr;
+  a.lsel = mb ? c.take<uint32_t>(nm * K * 4) : nullptr;
+  a.leq = mb ? c.take<uint32_t>(nm * K * kListEq) : nullptr;
+  a.leqn = mb ? c.take<uint32_t>(nm * K) : nullptr;
+  a.lok = mb ? c.take<uint8_t>(nm * K) : nullptr;
   a.lst = list ? c.take<uint2>(4 * N + 256 * (int64_t)K * nm) : nullptr;
   a.lcnt = list ? c.take<uint32_t>(nm * K * kAbovePad) : nullptr;
   a.lkb = list ? c.take<uint32_t>(nm * K) : nullptr;
@@ -1643,7 +1854,19 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     hipLaunchKernelGGL(sa_list_layout_kernel, dim3(1), dim3(1), 0, st, a);
   }
   auto launch_round = [&](hipStream_t q, bool count, bool lean) {
-    if (a.lst) hipLaunchKernelGGL(sa_list_round_kernel, dim3((unsigned)(n_multi * a.K)), dim3(kLT), 0, q, a);
+    if (a.lst && a.lmb_chunks) {
+      const dim3 gw((unsigned)(n_multi * a.K)), gp((unsigned)((int64_t)n_multi * a.K * a.lmb_chunks));
+      hipLaunchKernelGGL(sa_mlist_init_kernel, gw, dim3(256), 0, q, a);
+      hipLaunchKernelGGL(sa_mlist_pass_kernel<0>, gp, dim3(256), 0, q, a);
+      hipLaunchKernelGGL(sa_mlist_select_kernel<0>, gw, dim3(64), 0, q, a);
+      hipLaunchKernelGGL(sa_mlist_pass_kernel<1>, gp, dim3(256), 0, q, a);
+      hipLaunchKernelGGL(sa_mlist_select_kernel<1>, gw, dim3(64), 0, q, a);
+      hipLaunchKernelGGL(sa_mlist_pass_kernel<2>, gp, dim3(256), 0, q, a);
+      hipLaunchKernelGGL(sa_mlist_eq_kernel, gw, dim3(kLT), 0, q, a);
+      hipLaunchKernelGGL(sa_mlist_pass_kernel<3>, gp, dim3(256), 0, q, a);
+    } else if (a.lst) {
+      hipLaunchKernelGGL(sa_list_round_kernel, dim3((unsigned)(n_multi * a.K)), dim3(kLT), 0, q, a);
+    }
     if (n_multi > 0) {
       if (vec) hipLaunchKernelGGL((sa_guess_hist_kernel<true>), gcw, dim3(256), 0, q, a);
       else hipLaunchKernelGGL((sa_guess_hist_kernel<false>), gcw, dim3(256), 0, q, a);

@@ -358,13 +358,15 @@ def test_sharded_balanced_fit_world1(tmp_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,k,half", [(200_000, 128, False), (100_000, 1280, True), (60_001, 1280, True)])
+@pytest.mark.parametrize("n,k,half", [(200_000, 128, False), (100_000, 1280, True), (60_001, 1280, True),
+                                      (600_000, 128, False), (800_001, 128, True)])
 def test_auction_bid_list_equals_sweep(n, k, half, monkeypatch):
     """List rounds (auction_seg.hip sa_list_round_kernel: a worker's threshold, tie ranks and bids from the jobs a
     sweep round listed, keys >= its threshold - 64, while the threshold stays above that base) give the sweep's
     assignment and round count (RQSID_AUCTION_LIST=0) on the level-0 (K = 128) and candidate-fit (K = 1280,
-    fp16 cdist) shapes, with the retention (round < 100) and leftover (round > 1000, N % K != 0) rules; times
-    both (printed)."""
+    fp16 cdist) shapes, with the retention (round < 100) and leftover (round > 1000, N % K != 0) rules; above
+    4096 jobs per worker the default is the multi-block form (sa_mlist_*), checked against the sweep and the
+    one-block form (RQSID_AUCTION_LIST=2); times all (printed)."""
     import time
     x = synth.small_mixture(n, m=3000, seed=k)
     x /= np.linalg.norm(x, axis=1, keepdims=True)
@@ -372,7 +374,7 @@ def test_auction_bid_list_equals_sweep(n, k, half, monkeypatch):
     c = xg[torch.from_numpy(np.random.default_rng(k).choice(n, k, replace=False)).to(DEV)] * 0.9
     w = ops.auction_scores(xg, c, half=half)
     out = {}
-    for mode in ("1", "0"):
+    for mode in ("1", "0", "2"):
         monkeypatch.setenv("RQSID_AUCTION_LIST", mode)
         ops.auction(w)
         torch.cuda.synchronize()
@@ -383,6 +385,7 @@ def test_auction_bid_list_equals_sweep(n, k, half, monkeypatch):
         out[mode] = (a.cpu().numpy(), rounds)
         print(f"n={n} k={k} list={mode}: {rounds} rounds, {dt * 1e3 / rounds:.3f} ms/round")
     assert np.array_equal(out["1"][0], out["0"][0]) and out["1"][1] == out["0"][1]
+    assert np.array_equal(out["2"][0], out["0"][0]) and out["2"][1] == out["0"][1]
     if n % k:
         assert out["1"][1] == 1002
 
