@@ -359,14 +359,14 @@ def test_sharded_balanced_fit_world1(tmp_path):
 
 
 @pytest.mark.parametrize("n,k,half", [(200_000, 128, False), (100_000, 1280, True), (60_001, 1280, True),
-                                      (600_000, 128, False), (800_001, 128, True)])
+                                      (800_001, 128, True), (1_100_001, 128, False)])
 def test_auction_bid_list_equals_sweep(n, k, half, monkeypatch):
     """List rounds (auction_seg.hip sa_list_round_kernel: a worker's threshold, tie ranks and bids from the jobs a
     sweep round listed, keys >= its threshold - 64, while the threshold stays above that base) give the sweep's
     assignment and round count (RQSID_AUCTION_LIST=0) on the level-0 (K = 128) and candidate-fit (K = 1280,
     fp16 cdist) shapes, with the retention (round < 100) and leftover (round > 1000, N % K != 0) rules; above
-    4096 jobs per worker the default is the multi-block form (sa_mlist_*), checked against the sweep and the
-    one-block form (RQSID_AUCTION_LIST=2); times all (printed)."""
+    8192 jobs per worker (one segment) the default is the multi-block form (sa_mlist_*), checked against the
+    sweep and the one-block form (RQSID_AUCTION_LIST=2); lists are built from round 32 on; times all (printed)."""
     import time
     x = synth.small_mixture(n, m=3000, seed=k)
     x /= np.linalg.norm(x, axis=1, keepdims=True)
