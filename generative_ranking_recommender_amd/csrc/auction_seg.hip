@@ -1249,8 +1249,7 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
   const int sg = a.mseg[r];
   if (!(a.flag[sg] & kLive)) return;
   __shared__ uint32_t hst[256];
-  __shared__ uint32_t eqj[kListEq];
-  __shared__ uint32_t sh[4];  // bin, above, T, need | number of equal values
+  __shared__ uint32_t sh[4];  // bin, above, T, need | radix-select bin and rank
   const int tid = threadIdx.x;
   const int counter = *a.round_dev;
   const uint32_t cap = (uint32_t)a.lcs[r];
@@ -1311,37 +1310,49 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
   __syncthreads();
   const uint32_t T = sh[2], need = sh[3];
   if (T < kb) return fail_list();  // (cannot happen with >= jpw + 1 values >= kb; kept as a guard)
-  // the jobs of the values equal to T, ascending (only `need` of them bid; none when need == 0)
+  // the first `need` of the values equal to T in job order bid: J = the need-th smallest job index among
+  // them, by a radix select over the index bytes (no sort, no bound on the number of equal values: fp16
+  // half scores put thousands of a worker's jobs on one value)
+  uint32_t J = 0;
   if (need) {
-    for (uint32_t i = tid; i < n; i += kLT) {
-      const uint2 e = L[i];
-      if ((e.y >> 16) == T) {
-        const uint32_t q = atomicAdd(&sh[0], 1u);
-        if (q < (uint32_t)kListEq) eqj[q] = e.x;
+    uint32_t rank = need;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      __syncthreads();
+      if (tid < 256) hst[tid] = 0;
+      __syncthreads();
+      for (uint32_t i = tid; i < n; i += kLT) {
+        const uint2 e = L[i];
+        if ((e.y >> 16) == T && (shift == 24 || (e.x >> (shift + 8)) == J))
+          atomicAdd(&hst[(e.x >> shift) & 255u], 1u);
       }
-    }
-  }
-  __syncthreads();
-  const uint32_t neq = sh[0];
-  if (neq > (uint32_t)kListEq) return fail_list();
-  uint32_t m = 1;
-  while (m < neq) m <<= 1;
-  for (uint32_t i = neq + tid; i < m; i += kLT) eqj[i] = 0xFFFFFFFFu;
-  __syncthreads();
-  for (uint32_t kk = 2; kk <= m; kk <<= 1)  // bitonic sort of the equal values' jobs
-    for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
-      for (uint32_t i = tid; i < m; i += kLT) {
-        const uint32_t p = i ^ jj;
-        if (p > i) {
-          const uint32_t x = eqj[i], y = eqj[p];
-          if ((x > y) == ((i & kk) == 0)) {
-            eqj[i] = y;
-            eqj[p] = x;
+      __syncthreads();
+      if (tid < 64) {  // ascending walk: the bin holding the rank-th smallest
+        const uint32_t h0 = hst[4 * tid], h1 = hst[4 * tid + 1], h2 = hst[4 * tid + 2], h3 = hst[4 * tid + 3];
+        const uint32_t own = h0 + h1 + h2 + h3;
+        uint32_t inc = own;  // inclusive prefix over lanes <= tid
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+          if (tid >= o) inc += y;
+        }
+        const unsigned long long m = __ballot(inc >= rank);
+        const int Ln = m ? __ffsll((long long)m) - 1 : 63;
+        if (tid == Ln) {
+          uint32_t acc = inc - own;  // strictly below this lane's bins
+          const uint32_t hv[4] = {h0, h1, h2, h3};
+          int q = 0;
+          for (; q < 3; ++q) {
+            if (acc + hv[q] >= rank) break;
+            acc += hv[q];
           }
+          sh[0] = (uint32_t)(4 * Ln + q);
+          sh[1] = rank - acc;
         }
       }
       __syncthreads();
+      J = (J << 8) | sh[0];
+      rank = sh[1];
     }
+  }
   const uint16_t eps = a.eps[sg];
   const _Float16 epsh = __builtin_bit_cast(_Float16, eps);
   const _Float16 vT = __builtin_bit_cast(_Float16, okey_inv(T));
@@ -1353,13 +1364,8 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
     if (k > T) {
       const _Float16 x = __builtin_bit_cast(_Float16, okey_inv(k));
       bid = __builtin_bit_cast(uint16_t, (_Float16)((_Float16)(x - vT) + epsh));
-    } else if (k == T && need) {
-      uint32_t lo = 0, hi = neq;  // rank of j among the equal values' jobs
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (eqj[mid] < j) lo = mid + 1; else hi = mid;
-      }
-      if (lo < need) bid = eps;
+    } else if (k == T && need && j <= J) {
+      bid = eps;
     }
     if (ret && a.hb[j] == w) bid = eps;  // retention: the previous winner bids eps on its job
     if (bid) atomicMax(&a.key[j], (bid << 16) | (0xFFFFu - (uint32_t)w));
