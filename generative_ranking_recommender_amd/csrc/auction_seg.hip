@@ -20,6 +20,8 @@
 // threshold left the bin takes the exact two-pass selection and a tie-count sweep in the same round.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 
 #include "internal.h"
 
@@ -112,15 +114,22 @@ struct SegAuction {
   uint32_t* leq;                 // [n_multi*K][kListEq]
   uint32_t* leqn;                // [n_multi*K]
   uint8_t* lok;                  // [n_multi*K]
+  uint32_t* lany;                // [1] some worker's list failed this round (0: the sweep kernels exit at once)
+  int32_t ldelta;                // keys below last round's threshold a list keeps (RQSID_LIST_DELTA, 1..128)
+  uint32_t* lstat;               // [8] list-round verdict counts (RQSID_LIST_STATS=1; null otherwise): ok, no
+                                 // list, overflow, leftover round, threshold below the base, too few values,
+                                 // too many ties (multi-block)
 };
 constexpr int64_t kListMaxJpw = 16384;  // one-block list rounds only while the average jobs per worker per segment is at most this
 constexpr int64_t kListBlockJpw = 8192;  // one wide segment above this many jobs per worker: multi-block list rounds
 // lists are built from this round on: an auction whose N is a multiple of K settles in a few dozen rounds,
 // where building lists costs more than they save (K=128 x 10M, 24 rounds: 4.93 against 3.26 ms per round);
-// the 1002-round auctions (N % K != 0) run lists for the rest
+// the 1002-round auctions (N % K != 0) run lists for the rest.  Starting one-block lists at round 1 was
+// measured worse (K=2560 x 6.25M 2.07 -> 2.19 ms per round, K=1280 x 10M 1.99 -> 2.43): thresholds move
+// fast in the first rounds and the lists overflow, so those rounds pay the list pass and the sweep)
 constexpr int kListStart = 32;
 constexpr int kMCH = 2048;               // list entries per block of a multi-block list round
-constexpr int kListDelta = 64;   // keys below last round's threshold kept in the bid list
+constexpr int kListDelta = 64;   // default keys below last round's threshold kept in the bid list
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ off, int n_seg, int64_t i) {
   int lo = 0, hi = n_seg - 1;  // last s with off[s] <= i
@@ -478,9 +487,17 @@ __device__ __forceinline__ void guess_values(const ChunkScores& cs, const LaneJo
 
 // the list slot of each worker's values: d >= dlist (d as in guess_worker: the offset of the value's
 // key from the window base, 256 = above the window), i.e. keys >= T_prev - kListDelta
-__device__ __forceinline__ int32_t list_dmin(uint32_t T) {
+__device__ __forceinline__ int32_t list_dmin(uint32_t T, int32_t delta) {
   if (T == 0) return 0x7FFFFFFF;  // no threshold yet (round 0: every worker takes the exact passes)
-  return max(0, (int32_t)(T & 0xFFFFu) - kListDelta - window_base(T));
+  return max(0, (int32_t)(T & 0xFFFFu) - delta - window_base(T));
+}
+
+// list verdict statistics (diagnostics only: RQSID_LIST_STATS=1)
+__device__ __forceinline__ void list_stat(const SegAuction& a, int why) {
+  if (a.lstat) atomicAdd(&a.lstat[why], 1u);
+}
+__device__ __forceinline__ int list_fail_why(uint32_t n, uint32_t cap, int counter) {
+  return n == 0 ? 1 : n > cap ? 2 : counter > 1000 ? 3 : 4;
 }
 
 // Append this block's values of the list range to their workers' lists: the window histogram gives each
@@ -501,7 +518,7 @@ __device__ __forceinline__ void list_append(const SegAuction& a, const ChunkInfo
     int32_t dm = 0;
     uint32_t part = 0;
     if (g < nw) {
-      dm = list_dmin(a.sel[((int64_t)ci.s * a.K + w0 + g) * 4 + 2]);
+      dm = list_dmin(a.sel[((int64_t)ci.s * a.K + w0 + g) * 4 + 2], a.ldelta);
       for (int sl = q * 16; sl < q * 16 + 16; ++sl) part += sl >= dm ? h[g * kGStride + sl] : 0u;
       if (q == 0 && dm <= 256) part += h[g * kGStride + 256];  // (no threshold yet: nothing listed)
     }
@@ -540,6 +557,7 @@ __device__ __forceinline__ void list_append(const SegAuction& a, const ChunkInfo
 
 template <bool VEC>
 __global__ __launch_bounds__(256) void sa_guess_hist_kernel(SegAuction a) {
+  if (a.lany && !*a.lany) return;  // every list held this round (lany: sa_list_round_kernel)
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
   if (!(f & kLive) || (f & kSingle)) return;
@@ -1107,6 +1125,7 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
 #endif
 template <bool VEC>
 __global__ __launch_bounds__(256) RQ_BID_ATTR void sa_bid_kernel(SegAuction a) {
+  if (a.lany && a.n_multi == a.S && !*a.lany) return;  // every list held (one-chunk segments have none)
   const int counter = *a.round_dev;
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   const uint8_t f = a.flag[ci.s];
@@ -1261,10 +1280,14 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
   auto fail_list = [&]() {
     if (tid == 0) {
       a.lbad[hw] = 1;
+      *a.lany = 1;
       a.lcnt[hw * kAbovePad] = 0;  // the sweep's guessed pass rebuilds it
     }
   };
-  if (n == 0 || n > cap || counter > 1000 || a.sel[sw * 4 + 2] < kb) return fail_list();
+  if (n == 0 || n > cap || counter > 1000 || a.sel[sw * 4 + 2] < kb) {
+    if (tid == 0) list_stat(a, list_fail_why(n, cap, counter));
+    return fail_list();
+  }
   if (tid < 256) hst[tid] = 0;
   __syncthreads();
   // pass 1: this round's value keys (raw score, cost, last winner), kept in the entries' upper 16 bits so
@@ -1288,7 +1311,10 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
   }
   __syncthreads();
   const uint32_t b1 = sh[0];
-  if (b1 == 0xFFFFFFFFu) return fail_list();  // fewer than jpw + 1 values at or above the list base
+  if (b1 == 0xFFFFFFFFu) {  // fewer than jpw + 1 values at or above the list base
+    if (tid == 0) list_stat(a, 5);
+    return fail_list();
+  }
   __syncthreads();
   if (tid < 256) hst[tid] = 0;
   __syncthreads();
@@ -1377,6 +1403,7 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
     sel[2] = T;
     sel[3] = need;
     a.lbad[hw] = 0;
+    list_stat(a, 0);
   }
 }
 
@@ -1387,6 +1414,7 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
 __device__ __forceinline__ void mlist_fail(const SegAuction& a, int64_t hw) {
   a.lok[hw] = 0;
   a.lbad[hw] = 1;
+  *a.lany = 1;
   a.lcnt[hw * kAbovePad] = 0;  // the sweep's guessed pass rebuilds it
 }
 
@@ -1407,8 +1435,12 @@ __global__ __launch_bounds__(256) void sa_mlist_init_kernel(SegAuction a) {
     const int counter = *a.round_dev;
     const int64_t sw = (int64_t)sg * a.K + w;
     a.leqn[hw] = 0;
-    if (n == 0 || n > cap || counter > 1000 || a.sel[sw * 4 + 2] < kb) mlist_fail(a, hw);
-    else a.lok[hw] = 1;
+    if (n == 0 || n > cap || counter > 1000 || a.sel[sw * 4 + 2] < kb) {
+      list_stat(a, list_fail_why(n, cap, counter));
+      mlist_fail(a, hw);
+    } else {
+      a.lok[hw] = 1;
+    }
   }
 }
 
@@ -1503,7 +1535,10 @@ __global__ __launch_bounds__(64) void sa_mlist_select_kernel(SegAuction a) {
     uint32_t tot = h[4 * lane] + h[4 * lane + 1] + h[4 * lane + 2] + h[4 * lane + 3];
     for (int o = 32; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o);
     if (tot < jpw + 1) {  // fewer than jpw + 1 values at or above the list base
-      if (lane == 0) mlist_fail(a, hw);
+      if (lane == 0) {
+        list_stat(a, 5);
+        mlist_fail(a, hw);
+      }
       return;
     }
     uint32_t b = 0, above = 0;
@@ -1536,7 +1571,10 @@ __global__ __launch_bounds__(kLT) void sa_mlist_eq_kernel(SegAuction a) {
   const uint32_t T = a.lsel[hw * 4 + 2], need = a.lsel[hw * 4 + 3];
   const uint32_t neq = need ? a.leqn[hw] : 0u;
   if (neq > (uint32_t)kListEq) {
-    if (tid == 0) mlist_fail(a, hw);
+    if (tid == 0) {
+      list_stat(a, 6);
+      mlist_fail(a, hw);
+    }
     return;
   }
   uint32_t* const g = a.leq + hw * kListEq;
@@ -1568,6 +1606,7 @@ __global__ __launch_bounds__(kLT) void sa_mlist_eq_kernel(SegAuction a) {
     sel[2] = T;
     sel[3] = need;
     a.lbad[hw] = 0;
+    list_stat(a, 0);
   }
 }
 
@@ -1599,6 +1638,7 @@ __global__ __launch_bounds__(256) void sa_round_end_kernel(SegAuction a, int cou
     *a.round_dev += 1;
     if (a.any_miss) *a.any_miss = 0;  // for the next round's select_guess (a store at the top of the guessed
                                       // pass would turn its uniform loads into vector loads)
+    if (a.lany) *a.lany = 0;          // (the next round's list pass sets it for any failed list)
   }
 
   uint32_t live = 0;
@@ -1749,6 +1789,11 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.lbad = list ? c.take<uint8_t>(nm * K) : nullptr;
   a.loff = list ? c.take<int64_t>(nm) : nullptr;
   a.lcs = list ? c.take<int32_t>(nm) : nullptr;
+  a.lany = list ? c.take<uint32_t>(1) : nullptr;
+  const char* ed = getenv("RQSID_LIST_DELTA");
+  a.ldelta = ed ? std::min(128, std::max(1, atoi(ed))) : kListDelta;
+  const char* es = getenv("RQSID_LIST_STATS");
+  a.lstat = list && es && atoi(es) ? c.take<uint32_t>(8) : nullptr;
 }
 
 }  // namespace
@@ -1863,7 +1908,10 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
         fill_async(a.lbad, 1, (size_t)n_multi * n_workers, st) != hipSuccess)
       return fail(RQSID_E_LAUNCH, "seg_auction: memset");
     hipLaunchKernelGGL(sa_list_layout_kernel, dim3(1), dim3(1), 0, st, a);
+    if (fill_async(a.lany, 0, 4, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "seg_auction: memset");
+    if (a.lstat && fill_async(a.lstat, 0, 32, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   }
+  int n_lean = 0, n_replay = 0, n_full = 0;  // (RQSID_LIST_STATS) round blocks by kind
   auto launch_round = [&](hipStream_t q, bool count, bool lean) {
     if (a.lst && a.lmb_chunks) {
       const dim3 gw((unsigned)(n_multi * a.K)), gp((unsigned)((int64_t)n_multi * a.K * a.lmb_chunks));
@@ -1928,6 +1976,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   for (int done = 0; rc == RQSID_OK && (max_rounds <= 0 || done < max_rounds);) {
     const int n = max_rounds > 0 ? std::min(kPoll, max_rounds - done) : kPoll;
     const bool lean = try_lean && exec_lean && n == kPoll;
+    (lean ? n_lean : n_full) += 1;
     if (lean) {
       hipLaunchKernelGGL(sa_snapshot_kernel, dim3(gsnap), dim3(256), 0, st, a, out_assign, n_jobs, 0);
       if (fill_async(a.live_count + 2, 0, 4, st) != hipSuccess || hipGraphLaunch(exec_lean, st) != hipSuccess) {
@@ -1962,6 +2011,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
         break;
       }
       try_lean = false;
+      ++n_replay;
     } else {
       try_lean = n_multi > 0;
     }
@@ -1972,6 +2022,14 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   }
   if (exec_lean) (void)hipGraphExecDestroy(exec_lean);
   if (exec) (void)hipGraphExecDestroy(exec);
+  if (rc == RQSID_OK && a.lstat) {
+    uint32_t v[8] = {};
+    if (hipMemcpyAsync(v, a.lstat, 32, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess)
+      fprintf(stderr,
+              "rqsid list stats K=%d N=%lld: ok %u none %u overflow %u leftover %u drift %u few %u ties %u | "
+              "blocks lean %d full %d replayed %d\n",
+              n_workers, (long long)n_jobs, v[0], v[1], v[2], v[3], v[4], v[5], v[6], n_lean, n_full, n_replay);
+  }
   return rc;
 }
 
