@@ -62,7 +62,8 @@ struct SegAuction {
   uint32_t* have;                // [S] jobs with a bidder this round
   int32_t* rounds;               // [S] rounds run (device)
   int32_t* round_dev;            // [1] the current round (device, so a captured block of rounds replays)
-  uint32_t* live_count;          // [3]: live segments, multi-chunk segments, a miss in a lean block
+  uint32_t* live_count;          // [4]: live segments, multi-chunk segments, a miss in a lean block, a list
+                                 // that failed in this block (a list-only block is then replayed)
   uint16_t* cost;                // [N]
   int32_t* hb;                   // [N]
   uint8_t* nobid;                // [N]
@@ -115,6 +116,7 @@ struct SegAuction {
   uint32_t* leqn;                // [n_multi*K]
   uint8_t* lok;                  // [n_multi*K]
   uint32_t* lany;                // [1] some worker's list failed this round (0: the sweep kernels exit at once)
+  int32_t lstart;                // first round that builds lists (kListStart; RQSID_LIST_START)
   int32_t ldelta;                // keys below last round's threshold a list keeps (RQSID_LIST_DELTA, 1..128)
   uint32_t* lstat;               // [8] list-round verdict counts (RQSID_LIST_STATS=1; null otherwise): ok, no
                                  // list, overflow, leftover round, threshold below the base, too few values,
@@ -128,6 +130,12 @@ constexpr int64_t kListBlockJpw = 8192;  // one wide segment above this many job
 // measured worse (K=2560 x 6.25M 2.07 -> 2.19 ms per round, K=1280 x 10M 1.99 -> 2.43): thresholds move
 // fast in the first rounds and the lists overflow, so those rounds pay the list pass and the sweep)
 constexpr int kListStart = 32;
+// ... and from round 16 at K >= 1024 (candidate fits: a sweep there reads K x N fp16 scores, up to 32 GB, so
+// earlier lists pay even with the overflow failures of the first rounds): K=2560 x 6.25M 1.69 -> 1.34 ms per
+// round, K=1280 x 10M 1.71 -> 1.50, K=1280 x 1M 0.190 -> 0.163; at K=128 x 1M round 16 lost (0.105 -> 0.137),
+// and a settling K=1280 x 1.28M auction (27 rounds) 4.04 -> 4.83 (profiles/r4_list_start.jsonl)
+constexpr int kListStartWide = 16;
+constexpr int kListWideK = 1024;
 constexpr int kMCH = 2048;               // list entries per block of a multi-block list round
 constexpr int kListDelta = 64;   // default keys below last round's threshold kept in the bid list
 
@@ -610,7 +618,7 @@ __global__ __launch_bounds__(256) void sa_guess_hist_kernel(SegAuction a) {
     const uint32_t c = h[(i >> 8) * kStride + (i & 255)];
     if (c) atomicAdd(&a.hist[(hw0 + (i >> 8)) * 256 + (i & 255)], c);
   }
-  if (a.lst && *a.round_dev >= kListStart)  // (block-uniform)
+  if (a.lst && *a.round_dev >= a.lstart)  // (block-uniform)
     list_append<VEC>(a, ci, cs, lj, nc, addk, negbin, low && ci.nj < kCh, w0, nw, hw0, h);
 }
 
@@ -1281,6 +1289,7 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
     if (tid == 0) {
       a.lbad[hw] = 1;
       *a.lany = 1;
+      a.live_count[3] = 1;
       a.lcnt[hw * kAbovePad] = 0;  // the sweep's guessed pass rebuilds it
     }
   };
@@ -1415,6 +1424,7 @@ __device__ __forceinline__ void mlist_fail(const SegAuction& a, int64_t hw) {
   a.lok[hw] = 0;
   a.lbad[hw] = 1;
   *a.lany = 1;
+  a.live_count[3] = 1;
   a.lcnt[hw * kAbovePad] = 0;  // the sweep's guessed pass rebuilds it
 }
 
@@ -1790,6 +1800,8 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.loff = list ? c.take<int64_t>(nm) : nullptr;
   a.lcs = list ? c.take<int32_t>(nm) : nullptr;
   a.lany = list ? c.take<uint32_t>(1) : nullptr;
+  const char* ls = getenv("RQSID_LIST_START");
+  a.lstart = ls ? std::max(1, atoi(ls)) : K >= kListWideK ? kListStartWide : kListStart;
   const char* ed = getenv("RQSID_LIST_DELTA");
   a.ldelta = ed ? std::min(128, std::max(1, atoi(ed))) : kListDelta;
   const char* es = getenv("RQSID_LIST_STATS");
@@ -1911,8 +1923,14 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     if (fill_async(a.lany, 0, 4, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "seg_auction: memset");
     if (a.lstat && fill_async(a.lstat, 0, 32, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   }
-  int n_lean = 0, n_replay = 0, n_full = 0;  // (RQSID_LIST_STATS) round blocks by kind
-  auto launch_round = [&](hipStream_t q, bool count, bool lean) {
+  int n_lean = 0, n_replay = 0, n_full = 0, n_list = 0;  // (RQSID_LIST_STATS) round blocks by kind
+  // list-only rounds (one wide-segment auctions whose lists all held in the last block): the list pass,
+  // resolve and round end, without the guessed pass, selection and bid sweep, whose blocks all exit when
+  // every list holds but whose dispatch over total_chunks x K/16 blocks costs ~0.2 ms per kernel at K=2560
+  // over 6.25M jobs.  Such a block runs from a snapshot like a lean block and is replayed in full when any
+  // list failed in it (live_count[3]).
+  const bool list_only_ok = a.lst && !any_single;
+  auto launch_round = [&](hipStream_t q, bool count, bool lean, bool list_only = false) {
     if (a.lst && a.lmb_chunks) {
       const dim3 gw((unsigned)(n_multi * a.K)), gp((unsigned)((int64_t)n_multi * a.K * a.lmb_chunks));
       hipLaunchKernelGGL(sa_mlist_init_kernel, gw, dim3(256), 0, q, a);
@@ -1925,6 +1943,11 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
       hipLaunchKernelGGL(sa_mlist_pass_kernel<3>, gp, dim3(256), 0, q, a);
     } else if (a.lst) {
       hipLaunchKernelGGL(sa_list_round_kernel, dim3((unsigned)(n_multi * a.K)), dim3(kLT), 0, q, a);
+    }
+    if (list_only) {
+      hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, q, a, out_assign);
+      hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
+      return;
     }
     if (n_multi > 0) {
       if (vec) hipLaunchKernelGGL((sa_guess_hist_kernel<true>), gcw, dim3(256), 0, q, a);
@@ -1951,13 +1974,13 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
   };
   // capture blocks on a private stream (the caller's may be the null stream, which cannot capture)
-  auto capture = [&](bool lean) {
+  auto capture = [&](bool lean, bool list_only = false) {
     hipGraphExec_t ex = nullptr;
     hipStream_t cs = nullptr;
     hipGraph_t graph = nullptr;
     if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) == hipSuccess) {
       if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) == hipSuccess) {
-        for (int i = 0; i < kPoll; ++i) launch_round(cs, i == kPoll - 1, lean);
+        for (int i = 0; i < kPoll; ++i) launch_round(cs, i == kPoll - 1, lean, list_only);
         if (hipStreamEndCapture(cs, &graph) == hipSuccess && graph) {
           if (hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0) != hipSuccess) ex = nullptr;
           (void)hipGraphDestroy(graph);
@@ -1970,16 +1993,24 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   };
   hipGraphExec_t exec = capture(false);
   hipGraphExec_t exec_lean = n_multi > 0 && exec ? capture(true) : nullptr;
+  const char* elo = getenv("RQSID_LIST_ONLY");  // 0: no list-only blocks (A/B)
+  hipGraphExec_t exec_list = list_only_ok && exec_lean && !(elo && atoi(elo) == 0) ? capture(true, true) : nullptr;
+  bool try_list = false;
   const unsigned gsnap = (unsigned)grid_cap(cdiv(std::max<int64_t>(n_jobs, (int64_t)n_seg * n_workers * 4), 256), 4096);
   if (fill_async(a.live_count, 0, 4, st) != hipSuccess) rc = fail(RQSID_E_LAUNCH, "seg_auction: memset");
   bool try_lean = false;  // round 0 misses everywhere (thresholds start at key 0)
   for (int done = 0; rc == RQSID_OK && (max_rounds <= 0 || done < max_rounds);) {
     const int n = max_rounds > 0 ? std::min(kPoll, max_rounds - done) : kPoll;
-    const bool lean = try_lean && exec_lean && n == kPoll;
-    (lean ? n_lean : n_full) += 1;
-    if (lean) {
+    const bool lonly = try_list && exec_list && n == kPoll;
+    const bool lean = !lonly && try_lean && exec_lean && n == kPoll;
+    (lonly ? n_list : lean ? n_lean : n_full) += 1;
+    if (fill_async(a.live_count + 2, 0, 8, st) != hipSuccess) {
+      rc = fail(RQSID_E_LAUNCH, "seg_auction: memset");
+      break;
+    }
+    if (lonly || lean) {
       hipLaunchKernelGGL(sa_snapshot_kernel, dim3(gsnap), dim3(256), 0, st, a, out_assign, n_jobs, 0);
-      if (fill_async(a.live_count + 2, 0, 4, st) != hipSuccess || hipGraphLaunch(exec_lean, st) != hipSuccess) {
+      if (hipGraphLaunch(lonly ? exec_list : exec_lean, st) != hipSuccess) {
         rc = fail(RQSID_E_LAUNCH, "seg_auction: graph launch");
         break;
       }
@@ -1992,13 +2023,14 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
       for (int i = 0; i < n; ++i) launch_round(st, i == n - 1, false);
     }
     if ((rc = check_launch("seg_auction_round"))) break;
-    if (hipMemcpyAsync(host, a.live_count, 12, hipMemcpyDeviceToHost, st) != hipSuccess ||
+    if (hipMemcpyAsync(host, a.live_count, 16, hipMemcpyDeviceToHost, st) != hipSuccess ||
         fill_async(a.live_count, 0, 4, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
       rc = fail(RQSID_E_LAUNCH, "seg_auction: readback");
       break;
     }
-    if (lean && host[2]) {
-      // a worker missed inside the lean block: back to its start, replay it with the exact passes
+    if ((lean && host[2]) || (lonly && host[3])) {
+      // a worker missed inside the lean block, or a list failed inside the list-only block: back to its
+      // start, replay it with the exact passes
       hipLaunchKernelGGL(sa_snapshot_kernel, dim3(gsnap), dim3(256), 0, st, a, out_assign, n_jobs, 1);
       if (hipGraphLaunch(exec, st) != hipSuccess) {
         rc = fail(RQSID_E_LAUNCH, "seg_auction: graph launch");
@@ -2011,15 +2043,18 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
         break;
       }
       try_lean = false;
+      try_list = false;
       ++n_replay;
     } else {
       try_lean = n_multi > 0;
+      try_list = host[3] == 0;  // every list held through this block
     }
     done += n;
     if (host[0] == 0) break;
     if (max_rounds > 0 && done >= max_rounds)
       rc = fail(RQSID_E_LAUNCH, "seg_auction: %u segments still bidding after %d rounds", host[0], max_rounds);
   }
+  if (exec_list) (void)hipGraphExecDestroy(exec_list);
   if (exec_lean) (void)hipGraphExecDestroy(exec_lean);
   if (exec) (void)hipGraphExecDestroy(exec);
   if (rc == RQSID_OK && a.lstat) {
@@ -2027,8 +2062,8 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     if (hipMemcpyAsync(v, a.lstat, 32, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess)
       fprintf(stderr,
               "rqsid list stats K=%d N=%lld: ok %u none %u overflow %u leftover %u drift %u few %u ties %u | "
-              "blocks lean %d full %d replayed %d\n",
-              n_workers, (long long)n_jobs, v[0], v[1], v[2], v[3], v[4], v[5], v[6], n_lean, n_full, n_replay);
+              "blocks list-only %d lean %d full %d replayed %d\n",
+              n_workers, (long long)n_jobs, v[0], v[1], v[2], v[3], v[4], v[5], v[6], n_list, n_lean, n_full, n_replay);
   }
   return rc;
 }
