@@ -337,6 +337,8 @@ def batched_fit(X: torch.Tensor, layout: "ops.SegmentLayout", n_clusters: int, i
         frozen = torch.from_numpy(~active).to(dev)
         new[frozen.repeat_interleave(K)] = prev[frozen.repeat_interleave(K)]
         centers = new.contiguous()
+        if TRACE is None:
+            w = None  # the auction's score matrix is dead unless traced: free it before the loss scores
         loss = None
         if min_loss_mode:
             if half:  # argmin of the fp16 distances, first index (:327-329 with pairwise_distance_half)
@@ -428,8 +430,9 @@ def fit_segments(X: torch.Tensor, sizes, n_clusters: int, iter_limits, inits=Non
     start, restarts, guess, solo = 0, 0, 0, False
     while start < S:
         # after an attempt that kept nothing (the window's first segment drew out of the reference's order)
-        # that segment runs alone, which is exact by construction; the restart budget counts only attempts
-        # that made partial progress
+        # that segment runs alone, which is exact by construction; every multi-segment window that stopped
+        # short (kept nothing or part) counts against the restart budget, so a run of such windows falls
+        # back to one segment at a time after max_restarts instead of re-running every remaining segment
         stop = start + 1 if (solo or restarts > max_restarts) else S
         np_states, seg_inits = [], []
         for s in range(start, stop):
@@ -491,7 +494,7 @@ def fit_segments(X: torch.Tensor, sizes, n_clusters: int, iter_limits, inits=Non
         # next attempt: this rank's draws start after the lower ranks' draws of segments >= good
         guess = int(sum(int((e[:, 0] >= good).sum()) for r, e in enumerate(ev_all) if comm is not None and r < comm.rank))
         solo = good == start
-        if start < good < stop:
+        if good < stop and stop - start > 1:
             restarts += 1
         start = good
         window += 1

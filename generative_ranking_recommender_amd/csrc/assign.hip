@@ -914,6 +914,14 @@ __device__ __forceinline__ double half_sum(double v) {
 // consecutive items are rows of one segment walking the same candidates, so a candidate row is read from
 // L2 once per block rather than once per row (the per-row arithmetic is the same code)
 constexpr int kOvfSlot = 56;  // workspace header int: overflow item count
+// workspace header int 60: error word of the counter-driven list writes (zeroed with the header by every
+// rqsid_assign call, read by rqsid_assign_error).  Each index such a write takes from a device counter is
+// checked against its slot's capacity; a write that would fall outside is dropped and its bit raised, so
+// a wrong count can only produce a reported error, never a store outside the workspace.
+constexpr int kErrSlot = 60;
+constexpr int kErrCompact = 1;   // sentinel compaction: more listed rows than n_rows
+constexpr int kErrOvfList = 2;   // overflow list: more overflow items than n_rows
+constexpr int kErrWorkIdx = 4;   // a work-list entry outside [0, n_rows)
 template <int RL, bool NORM>
 __global__ __launch_bounds__(256) void assign_rescore_half_kernel(AssignParams p, const int32_t* __restrict__ ovf_list,
                                                                   int mode) {
@@ -1074,7 +1082,15 @@ __global__ __launch_bounds__(256) void overflow_list_kernel(AssignParams p, int3
   const int64_t nitems = nitems_raw < p.work_cap ? nitems_raw : p.work_cap;
   for (int64_t it = (int64_t)blockIdx.x * 256 + threadIdx.x; it < nitems; it += (int64_t)gridDim.x * 256) {
     const int32_t idx = p.work_idx ? p.work_idx[it] : (int32_t)it;
-    if (p.work[idx].n == -1) ovf_list[atomicAdd(p.work_count + kOvfSlot, 1)] = idx;
+    if ((uint32_t)idx >= (uint32_t)p.work_cap) {  // a list entry outside work[]: never dereferenced
+      atomicOr(p.work_count + kErrSlot, kErrWorkIdx);
+      continue;
+    }
+    if (p.work[idx].n == -1) {
+      const int pos = atomicAdd(p.work_count + kOvfSlot, 1);
+      if (pos < p.work_cap) ovf_list[pos] = idx;
+      else atomicOr(p.work_count + kErrSlot, kErrOvfList);
+    }
   }
 }
 
@@ -1222,6 +1238,10 @@ __global__ __launch_bounds__(256) void assign_rescreen_kernel(AssignParams p, co
         cnt += ins ? 1 : 0;
       }
     }
+    // a NaN distance seen by any lane of the half (each lane checks only its own candidate) sends the
+    // whole row to the fp64 pass, which applies the reference's NaN rule
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) ovf = ovf || __shfl_xor((int)ovf, o) != 0;
     // the final list: entries still within the final U, ascending candidate order
     int m = 0;
     uint16_t outc[kMaxList];
@@ -1263,7 +1283,7 @@ __global__ __launch_bounds__(256) void tile_seg128_kernel(const int32_t* __restr
 constexpr int kCompactRows = 16384;
 __global__ __launch_bounds__(256) void sentinel_compact_kernel(const int32_t* __restrict__ out_global, int64_t n,
                                                                int32_t* __restrict__ work_count,
-                                                               int32_t* __restrict__ work_idx) {
+                                                               int32_t* __restrict__ work_idx, int64_t cap) {
   __shared__ int wcount[4], wbase[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * kCompactRows, r1 = min(n, r0 + kCompactRows);
@@ -1288,7 +1308,11 @@ __global__ __launch_bounds__(256) void sentinel_compact_kernel(const int32_t* __
     const int64_t i = i0 + lane;
     const bool need = i < r1 && out_global[i] == -2;
     const unsigned long long m = __ballot(need);
-    if (need) work_idx[pos + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+    if (need) {
+      const int64_t q = (int64_t)pos + __popcll(m & ((1ull << lane) - 1ull));
+      if (q < cap) work_idx[q] = (int32_t)i;
+      else atomicOr(work_count + kErrSlot, kErrCompact);
+    }
     pos += __popcll(m);
   }
 }
@@ -1484,7 +1508,8 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   p.den_in = den_in;
   p.den_out = den_out;
   const bool norm = res_normalize != 0;
-  if (fill_async(workspace, 0, 256, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "assign: memset");
+  // header ints [0, 60) per call; [60, 64) hold the sticky error word (kErrSlot), zeroed by the allocator
+  if (fill_async(workspace, 0, 4 * kErrSlot, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "assign: memset");
   const unsigned grid = (unsigned)((max_tiles + 7) / 8 * 8);  // XCD remap needs a multiple of 8
   // Measured on MI355X (tools/screen_sweep.py): independent blocks per CU beat ring depth: NT4 with
   // S=2 runs 3 blocks/CU, NT8 with S=2 runs 2 blocks/CU (RQSID_SCREEN_VARIANT=1/3 select the older
@@ -1541,7 +1566,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
     // re-score rows carry the sentinel -2 and their pass masks at work[row] (the 32-row tile offsets in
     // the compact-list area are dead by now); the expand pass makes them work items
     hipLaunchKernelGGL(sentinel_compact_kernel, dim3((unsigned)cdiv(n_rows, kCompactRows)), dim3(256), 0, st, out_global,
-                       n_rows, p.work_count, work_idx);
+                       n_rows, p.work_count, work_idx, n_rows);
     p.work_idx = work_idx;
     launch_resident_expand(p, tile_seg, t3, n_rows, st);
   } else if (use_stream) {
@@ -1551,7 +1576,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
     if ((rc = launch_stream_screen(p, nt, t3, res_levels, norm, tile_seg, work_idx, n_rows, shape, st))) return rc;
     if ((rc = check_launch("assign_stream"))) return rc;
     hipLaunchKernelGGL(sentinel_compact_kernel, dim3((unsigned)cdiv(n_rows, kCompactRows)), dim3(256), 0, st, out_global,
-                       n_rows, p.work_count, work_idx);
+                       n_rows, p.work_count, work_idx, n_rows);
     p.work_idx = work_idx;
   } else {
     if (n_segments > 1) {  // (tiles <= rows: the map fits its workspace slot)

@@ -827,11 +827,15 @@ class HierarchicalRQKMeans:
         codebooks or changing a centre tensor in place rebuilds it; train / load_model drop the cache, and
         ``invalidate_encoder`` does after an in-place edit of a numpy match matrix."""
         from .encode import LevelSemantics, RQEncoder
-        key = (bool(reference_quirks), tuple((id(c), getattr(c, "_version", 0)) for c in self.cluster_centers_list),
-               tuple(id(m) for m in self.match_matrices))
+        # the cache entry holds the objects themselves (not their id(), which a new object can reuse once the
+        # old one is freed) and compares them by identity, plus each tensor's in-place version counter
+        objs = (list(self.cluster_centers_list), list(self.match_matrices))
+        vers = (bool(reference_quirks), tuple(getattr(c, "_version", 0) for c in self.cluster_centers_list))
         cache = getattr(self, "_enc_cache", None)
-        if cache is not None and cache[0] == key:
-            return cache[1]
+        if cache is not None and cache[0] == vers and len(cache[1][0]) == len(objs[0]) and \
+                len(cache[1][1]) == len(objs[1]) and all(a is b for a, b in zip(cache[1][0], objs[0])) and \
+                all(a is b for a, b in zip(cache[1][1], objs[1])):
+            return cache[2]
         cfg = self.config
         L = len(cfg.layer_clusters)
         match = None
@@ -844,7 +848,7 @@ class HierarchicalRQKMeans:
                              residual_from_weighted=not reference_quirks)
         enc = RQEncoder([c.float() for c in self.cluster_centers_list], cfg.need_clusters, match=match,
                         group_dims=cfg.group_dims, weights=cfg.hierarchical_weights, semantics=sem, device=self.device)
-        self._enc_cache = (key, enc)
+        self._enc_cache = (vers, objs, enc)
         return enc
 
     def invalidate_encoder(self) -> None:

@@ -186,11 +186,18 @@ class AssignWorkspace:
     def __init__(self, n_rows: int, device):
         self.bytes = int(lib().rqsid_assign_workspace_bytes(n_rows))
         self.buf = torch.empty(self.bytes, dtype=torch.uint8, device=device)
+        self.buf[240:256].zero_()  # the sticky error word (include/rqsid.h)
         self.n_rows = n_rows
 
     def rescored(self) -> int:
         """Rows re-scored in fp64 by the last assign (host sync)."""
         return int(self.buf[:4].view(torch.int32).item())
+
+    def error(self) -> int:
+        """Sticky error word of every assign on this workspace (host sync; csrc/assign.hip kErrSlot):
+        bit 0 compaction past n_rows, bit 1 overflow list past n_rows, bit 2 a list entry outside work[].
+        Every such write is bounded by its slot's capacity; a non-zero word means one was dropped."""
+        return int(self.buf[240:244].view(torch.int32).item())
 
 
 @dataclass

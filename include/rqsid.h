@@ -102,7 +102,11 @@ int32_t rqsid_assign_tile_rows(void);
  *
  * Errors: RQSID_E_ARG / RQSID_E_WORKSPACE before any launch; RQSID_E_LAUNCH for a HIP launch failure
  * or, on the opt-in centre-resident screen (RQSID_SCREEN_VARIANT=6), when a wave's capped role wait
- * gave up (device error word read back after the call; the IDs it left are not returned as valid). */
+ * gave up (device error word read back after the call; the IDs it left are not returned as valid).
+ * Workspace bytes [240, 244) are a sticky error word the caller zeroes when it allocates the workspace
+ * (every call zeroes only [0, 240)): each list write whose index comes from a device counter (the
+ * re-score compaction, the overflow list) is bounded by its slot's capacity, and a write that would fall
+ * outside sets a bit here instead (1 compaction, 2 overflow list, 4 a list entry outside [0, n_rows)). */
 int64_t rqsid_assign_workspace_bytes(int64_t n_rows);
 int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row_index,
                  int32_t n_segments, const int32_t* seg_row_off, const int32_t* seg_tile_off,

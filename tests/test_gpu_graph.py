@@ -49,3 +49,32 @@ def test_encode_step_graph_replays_equal_eager():
     torch.cuda.synchronize()
     assert torch.equal(out, enc.encode(x))
     del g
+
+
+def test_encode_list_writes_stay_in_bounds():
+    """Every list write of rqsid_assign whose index comes from a device counter (the sentinel compaction
+    of the streamed screens, the overflow list of the fp32 re-screen) is bounded by its slot and raises a
+    bit of the workspace's sticky error word instead of writing past it (csrc/assign.hip kErrSlot).  PROD
+    codebooks, every level, eager and three back-to-back graph replays: the word stays 0."""
+    dev = torch.device("cuda", 0)
+    cb = synth.encode_codebooks(seed=99)
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], [128, 128, 256],
+                    match=torch.from_numpy(cb["match"]), semantics=HIERARCHICAL_TRAIN, device=dev)
+    x = torch.from_numpy(synth.mixture_rows(0, 100_000)).to(dev)
+    eager = enc.encode(x).clone()
+    assert enc._ws.error() == 0
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        enc.encode(x)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = enc.encode(x)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eager)
+    assert enc._ws.error() == 0
+    del g
