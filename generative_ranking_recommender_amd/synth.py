@@ -119,3 +119,28 @@ def codebooks_sha(cb: dict) -> str:
     for k in ("c0", "c1", "c2", "match"):
         h.update(np.ascontiguousarray(cb[k]).tobytes())
     return h.hexdigest()
+
+
+def tree_mixture(labels: np.ndarray, fan0: int, fan1: int, n_leaf: int, d: int = D_DEFAULT,
+                 scales=(4.0, 1.0, 0.2), noise: float = 0.01, seed: int = 0) -> np.ndarray:
+    """A 3-level tree of blobs for training-parity fixtures: row i with labels (a, b, c) is
+    ``A[a] + B[a, b] + C[c] + noise`` with |A| >> |B| >> |C| >> noise, so level 0 of a residual K-Means
+    separates a, its level-1 residuals (x - mean_a, normalised) separate b inside each parent, and the
+    level-2 residuals separate the GLOBAL leaf direction c.  B sums to zero over b for every a and C over
+    c, so the blob means are the tree's nodes.  Directions are Gaussian (random, nearly orthogonal at
+    D = 512), each offset scaled to its level's norm; float32."""
+    rng = np.random.default_rng(seed)
+
+    def dirs(k, scale):
+        v = rng.standard_normal((k, d))
+        return v / np.linalg.norm(v, axis=1, keepdims=True) * scale
+
+    a_ = dirs(fan0, scales[0])
+    b_ = dirs(fan0 * fan1, scales[1]).reshape(fan0, fan1, d)
+    b_ -= b_.mean(1, keepdims=True)
+    c_ = dirs(n_leaf, scales[2])
+    c_ -= c_.mean(0, keepdims=True)
+    lab = np.asarray(labels, dtype=np.int64)
+    e = rng.standard_normal((len(lab), d)) * (noise / np.sqrt(d))
+    x = a_[lab[:, 0]] + b_[lab[:, 0], lab[:, 1]] + c_[lab[:, 2]] + e
+    return x.astype(np.float32)

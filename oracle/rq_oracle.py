@@ -465,8 +465,10 @@ def auction_tie_certificate(job_and_worker_to_score: np.ndarray) -> dict:
     are compared; the first round where they differ is returned with ``tie_born`` = every differing
     selection is among jobs whose value equals that worker's (jpw+1)-th largest (the topk boundary),
     or, for the max over bidders, among equal bids.  After that round the trajectories legitimately
-    part.  Returns {"diverged", "round", "step", "tie_born", "torch", "stable"} (the two results; without
-    a divergence both are the lockstep run's)."""
+    part.  Two selections whose top-jpw job SETS agree are the same step even when a different one of
+    several equal values sits at position jpw+1: the bids (value - (jpw+1)-th value + eps on the top jpw)
+    are identical.  Returns {"diverged", "round", "step", "tie_born", "torch", "stable"} (the two results;
+    without a divergence both are the lockstep run's)."""
     s = np.asarray(job_and_worker_to_score, dtype=F32)
     num_jobs, num_workers = s.shape
     out = {"diverged": False, "round": -1, "step": None, "tie_born": True}
@@ -491,10 +493,12 @@ def auction_tie_certificate(job_and_worker_to_score: np.ndarray) -> dict:
         ti = _auction_select(value, jpw, "torch")
         si = _auction_select(value, jpw, "stable")
         for wk in range(num_workers):
+            # the bids depend on WHICH jobs are in the top jpw and on the (jpw+1)-th VALUE, not on which of
+            # several equal values sits at position jpw+1: only a different bid set parts the trajectories
             bt, bs = set(ti[wk, :-1].tolist()), set(si[wk, :-1].tolist())
-            if bt != bs or ti[wk, -1] != si[wk, -1]:
+            if bt != bs:
                 thr = value[wk, si[wk, -1]]
-                diff = (bt ^ bs) | {int(ti[wk, -1]), int(si[wk, -1])}
+                diff = bt ^ bs
                 return parted(round=counter, step="topk",
                               tie_born=bool(value[wk, ti[wk, -1]] == thr and all(value[wk, j] == thr for j in diff)))
         top_values = np.take_along_axis(value, ti, 1)

@@ -112,3 +112,39 @@ def half_inputs(g):
     for a, key in ((x, "x_sha"), (c, "c_sha"), (x2, "x2_sha"), (c2, "c2_sha")):
         checked(a, g[key])
     return x, c, x2, c2
+
+
+# Training fixtures whose reference run takes no tie-born step (tests/golden/make_golden.py g_exact,
+# tests/golden/exact_fixture.py): rows = synth.tree_mixture(labels), labels stored in exact.npz.
+EXACT_CASES = {
+    "hier": {"kind": "hier", "n": 2048, "tree_seed": 5, "label_seed": 7},
+    "simp": {"kind": "simp", "n": 2048, "tree_seed": 6, "label_seed": 8},
+    "k8": {"kind": "single", "n": 2048, "k": 8, "iter_limit": 5, "tree_seed": 9, "label_seed": 10},
+    "k128": {"kind": "single", "n": 12800, "k": 128, "iter_limit": 3, "tree_seed": 11, "label_seed": 12},
+}
+
+
+def exact_placeholder(tag):
+    """balanced random labels of the case's shape (the first pass of the draw recording)"""
+    spec = EXACT_CASES[tag]
+    rng = np.random.default_rng(spec["label_seed"] + 1000)
+    n = spec["n"]
+    if spec["kind"] == "single":
+        a = rng.permutation(np.repeat(np.arange(spec["k"]), n // spec["k"]))
+        return np.stack([a, np.zeros_like(a), np.zeros_like(a)], 1)
+    m = n // 64
+    lab = np.array([(a, b, 8 * ((a * 8 + b) % 2) + c) for a in range(8) for b in range(8) for c in range(8)
+                    for _ in range(m // 8)], dtype=np.int64)
+    return lab[rng.permutation(n)]
+
+
+def exact_rows(tag, labels, g=None):
+    spec = EXACT_CASES[tag]
+    lab = np.asarray(labels, dtype=np.int64)
+    if spec["kind"] == "single":
+        x = synth.tree_mixture(lab, spec["k"], 1, 1, seed=spec["tree_seed"])
+    else:
+        x = synth.tree_mixture(lab, 8, 8, 16, seed=spec["tree_seed"])
+    if g is not None:
+        checked(x, g[f"{tag}_x_sha"])
+    return x

@@ -452,6 +452,79 @@ def g_config0():
     save("config0", **out)
 
 
+# --- G-exact: trainer runs on which the reference's own fits take no tie-born step -------
+def _exact_labels(run, n, shape_fn, tries=4):
+    """labels at the fixed point of (record the reference's initialisation draws -> place the labels)"""
+    import exact_fixture as E
+    lab = shape_fn(None)
+    for _ in range(tries):
+        with E.DrawRecorder() as dr:
+            run(lab)
+        new = shape_fn(dr.draws)
+        if np.array_equal(new, lab):
+            return lab
+        lab = new
+    raise RuntimeError("draws did not reach a fixed point")
+
+
+def g_exact():
+    """tests/_data.EXACT_CASES: the SMALL_CFG hierarchical and simplified trainers and the single-level
+    configs[0] runs on tree-mixture rows whose every fit is clean (tests/golden/precertify.py: no auction
+    whose two tie rules give different results, no fp16 rounding flip that changes one).  Stores the
+    labels (the tests regenerate the rows with synth.tree_mixture) and the reference's outputs."""
+    import exact_fixture as E
+    import precertify as PC
+    from tests import _data
+    out = {}
+    for tag, spec in _data.EXACT_CASES.items():
+        n, kind = spec["n"], spec["kind"]
+        if kind == "single":
+            k = spec["k"]
+            cfg = dict(layer_clusters=[k], need_clusters=[k], embedding_dim=512, iter_limit=spec["iter_limit"])
+        else:
+            cfg = dict(SMALL_CFG)
+
+        def shape_fn(draws):
+            if draws is None:  # placeholder: balanced random labels
+                return _data.exact_placeholder(tag)
+            if kind == "single":
+                lab = E.single_labels(draws[0][2], n, spec["k"], seed=spec["label_seed"])
+                return np.stack([lab, np.zeros_like(lab), np.zeros_like(lab)], 1)
+            return E.hier_labels(draws, n, 8, 8, 16, 8, seed=spec["label_seed"])
+
+        def run(lab):
+            x = _data.exact_rows(tag, lab)
+            return (PC.run_hierarchical if kind == "hier" else PC.run_simplified)(x, cfg)
+
+        lab = _exact_labels(run, n, shape_fn)
+        x = _data.exact_rows(tag, lab)
+        m, ids, fits = run(lab)
+        bad = [f for f in fits if not f["clean"]]
+        assert not bad, PC.summary(fits)
+        out[f"{tag}_labels"] = lab.astype(np.int16)
+        out[f"{tag}_x_sha"] = np.array(synth.sha256(x))
+        out[f"{tag}_ids"] = ids
+        out[f"{tag}_fits"] = np.array(len(fits))
+        if kind == "hier":
+            for l in range(3):
+                out[f"{tag}_c{l}"] = m.cluster_centers_list[l].numpy()
+            out[f"{tag}_match"] = np.array(m.match_matrices[0], dtype=np.uint8)
+        else:
+            out[f"{tag}_c0"] = m.trained_kmeans_models[0].cluster_centers.numpy()
+            if kind == "simp":
+                out[f"{tag}_c1"] = m.middle_layer_centers.numpy()
+                out[f"{tag}_c2"] = m.final_layer_centers.numpy()
+                out[f"{tag}_match"] = m.dynamic_match_matrix.numpy().astype(np.uint8)
+            sids = [f"s{i:05d}" for i in range(n)]
+            with tempfile.TemporaryDirectory() as td:
+                o = os.path.join(td, "ids.jsonl")
+                m.save_semantic_ids(o)
+                raw = Path(o).read_bytes()
+            out[f"{tag}_jsonl_sha"] = np.array(synth.sha256(np.frombuffer(raw, dtype=np.uint8)))
+        print(tag, "clean fits:", len(fits))
+    save("exact", **out)
+
+
 # --- G-csv: loader skip rules (simplified :38-76) ----------------------------
 def g_csv():
     rows = [["a", "1", "2", "3", "4"], ["b"], ["c", "1", "x", "3", "4"], ["d", "1", "2", "3"],
@@ -473,6 +546,6 @@ def g_csv():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["assign", "residual", "update", "auction", "fit", "simplified",
-                             "hierarchical", "encode_prod", "csv", "dist_half", "trainer", "match", "config0"]
+                             "hierarchical", "encode_prod", "csv", "dist_half", "trainer", "match", "config0", "exact"]
     for w in which:
         globals()[f"g_{w}"]()

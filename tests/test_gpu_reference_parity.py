@@ -273,6 +273,105 @@ def test_simplified_train_certified_against_reference(golden, tracer, tmp_path):
            **{k: v for k, v in st.items() if k != "segments"})
 
 
+# ------------------------------------------------------------- exact-branch fixtures
+# tests/golden/exact.npz: tree-mixture rows (tests/_data.EXACT_CASES) on which the reference's own fits take
+# no tie-born step (tests/golden/precertify.py certified every auction of the reference run: its two tie
+# rules give the same result and no fp16 rounding flip changes it).  Here the per-segment rule must take its
+# EXACT branch everywhere: the north star's bound (centres within 1e-4, identical IDs) is asserted on a whole
+# trainer run, not only step by step.
+def _exact_case(golden, tag):
+    g = golden("exact")
+    return g, _data.exact_rows(tag, g[f"{tag}_labels"], g)
+
+
+def test_hierarchical_train_exact_against_reference(golden, tracer):
+    """HierarchicalRQKMeans.train (:368-537) on exact.npz's hier rows: no certified divergence in any traced
+    step, so level 0, every parent block, both candidate fits, the match matrix and every id equal the
+    reference's (centres within 1e-4)."""
+    g, x = _exact_case(golden, "hier")
+    seeded(42)
+    m = HierarchicalRQKMeans(HierarchicalRQKMeansConfig(**_data.SMALL_CFG), device=DEV)
+    res = m.train(x, resume=False)
+    ids = np.stack([t.cpu().numpy() for t in res["cluster_ids"]], 1).astype(np.int64)
+    st = _certify.certify_trace(tracer.events)
+    need = _data.SMALL_CFG["need_clusters"]
+    cents = [t.cpu().numpy() for t in m.cluster_centers_list]
+    ref_cents = [g["hier_c0"], g["hier_c1"], g["hier_c2"]]
+    match = np.asarray(m.match_matrices[0])
+    exact = _cascade(st, tracer.events, ids, g["hier_ids"], cents, ref_cents, need, match, g["hier_match"])
+    report("hierarchical_train_exact", exact=exact, agree_per_level=(ids == g["hier_ids"]).mean(0),
+           max_center_diff=[float(np.abs(a - b).max()) for a, b in zip(cents, ref_cents)],
+           **{k: v for k, v in st.items() if k != "segments"})
+    assert _no_step_diverged(st)
+    assert exact == {"level0": True, "parents": need[0], "candidates": True, "groups": True}, exact
+    assert np.array_equal(ids, g["hier_ids"])
+    for a, b in zip(cents, ref_cents):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4)
+    # predict (training semantics) of the trained model reproduces the training ids
+    assert np.array_equal(m.predict(x), ids)
+
+
+def test_simplified_train_exact_against_reference(golden, tracer, tmp_path):
+    """SimplifiedHierarchicalRQ.train (simplified…:176-245) through the CSV entry point on exact.npz's simp
+    rows: no certified divergence, every level's centres within 1e-4, the dynamic match matrix, every
+    song's ids and the jsonl bytes identical to the reference's."""
+    g, x = _exact_case(golden, "simp")
+    sids = [f"s{i:05d}" for i in range(len(x))]
+    p = tmp_path / "vec.csv"
+    rq_io.write_song_vectors(str(p), sids, x)
+    seeded(42)
+    m = SimplifiedHierarchicalRQ(HierarchicalRQKMeansConfig(**_data.SMALL_CFG), device=DEV)
+    m.train(str(p))
+    ids = np.array([m.semantic_ids[s] for s in sids], dtype=np.int64)
+    st = _certify.certify_trace(tracer.events)
+    need = _data.SMALL_CFG["need_clusters"]
+    cents = [m.trained_kmeans_models[0].cluster_centers.cpu().numpy(), m.middle_layer_centers.cpu().numpy(),
+             m.final_layer_centers.cpu().numpy()]
+    ref_cents = [g["simp_c0"], g["simp_c1"], g["simp_c2"]]
+    match = np.asarray(m.dynamic_match_matrix).astype(np.uint8)
+    exact = _cascade(st, tracer.events, ids, g["simp_ids"], cents, ref_cents, need, match, g["simp_match"])
+    out = tmp_path / "ids.jsonl"
+    m.save_semantic_ids(str(out))
+    same_bytes = synth.sha256(np.frombuffer(out.read_bytes(), dtype=np.uint8)) == str(g["simp_jsonl_sha"])
+    report("simplified_train_exact", exact=exact, agree_per_level=(ids == g["simp_ids"]).mean(0), jsonl=same_bytes,
+           max_center_diff=[float(np.abs(a - b).max()) for a, b in zip(cents, ref_cents)],
+           **{k: v for k, v in st.items() if k != "segments"})
+    assert _no_step_diverged(st)
+    assert exact == {"level0": True, "parents": need[0], "candidates": True, "groups": True}, exact
+    assert np.array_equal(ids, g["simp_ids"])
+    for a, b in zip(cents, ref_cents):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-4)
+    assert same_bytes
+
+
+@pytest.mark.parametrize("tag", ["k8", "k128"])
+def test_config0_single_level_exact_against_reference(golden, tracer, tag, tmp_path):
+    """BASELINE configs[0]'s single-level simplified run (layer_clusters = need = [K]) on exact.npz's rows:
+    no certified divergence, centres within 1e-4, every song's id and the jsonl bytes identical."""
+    g, x = _exact_case(golden, tag)
+    spec = _data.EXACT_CASES[tag]
+    k, it = spec["k"], spec["iter_limit"]
+    sids = [f"s{i:05d}" for i in range(len(x))]
+    p = tmp_path / "vec.csv"
+    rq_io.write_song_vectors(str(p), sids, x)
+    seeded(42)
+    m = SimplifiedHierarchicalRQ(HierarchicalRQKMeansConfig(layer_clusters=[k], need_clusters=[k], embedding_dim=512,
+                                                            iter_limit=it), device=DEV)
+    m.train(str(p))
+    ids = np.array([m.semantic_ids[s] for s in sids], dtype=np.int64)
+    st = _certify.certify_trace(tracer.events)
+    c = m.trained_kmeans_models[0].cluster_centers.cpu().numpy()
+    out = tmp_path / "ids.jsonl"
+    m.save_semantic_ids(str(out))
+    same_bytes = synth.sha256(np.frombuffer(out.read_bytes(), dtype=np.uint8)) == str(g[f"{tag}_jsonl_sha"])
+    report("config0_exact", tag=tag, identical=bool(np.array_equal(ids, g[f"{tag}_ids"])), jsonl=same_bytes,
+           max_center_diff=float(np.abs(c - g[f"{tag}_c0"]).max()), **{k2: v for k2, v in st.items() if k2 != "segments"})
+    assert _no_step_diverged(st) and st["steps"] >= 1
+    np.testing.assert_allclose(c, g[f"{tag}_c0"], rtol=1e-4, atol=1e-4)
+    assert np.array_equal(ids, g[f"{tag}_ids"])
+    assert same_bytes
+
+
 def test_candidate_fit_half_k1280_certified(tracer):
     """The last layer's candidate fits at their PROD width (hierarchical_rq_kmeans.py:792-801:
     KMeans(n_clusters=1280, balanced=True).fit(half=True)) on a small row set of normalised residual-like

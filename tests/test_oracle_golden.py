@@ -290,3 +290,36 @@ def test_config0_single_level_matches_reference(golden, tag):
                         dist_fn=O.torch_cdist_batched)
     np.testing.assert_allclose(c, g[f"{tag}_centers"], rtol=1e-5, atol=1e-5)
     assert np.array_equal(O.torch_cdist_batched(x, c).argmin(1), g[f"{tag}_ids"][:, 0])
+
+
+@pytest.mark.parametrize("tag", ["k8", "k128"])
+def test_config0_exact_fixture_matches_reference_with_either_tie_rule(golden, tag):
+    """tests/golden/exact.npz (the tree-mixture rows on which the reference's fits take no tie-born step):
+    the oracle's fit_by_min_loss reproduces the reference's centres and IDs with the reference's own
+    torch.topk tie choice AND with the lowest-index rule of the HIP kernels, and with numpy's summation
+    order as well as torch's -- the fixture pins the trainer, not an implementation detail."""
+    g = golden("exact")
+    x = _data.exact_rows(tag, g[f"{tag}_labels"], g)
+    spec = _data.EXACT_CASES[tag]
+    for dist in (O.torch_cdist_batched, O.cdist_f32):
+        torch.manual_seed(42)
+        rng = O.LegacyRNG(42, lambda n: torch.randint(n, (1,)).item())
+        c, _ = O.kmeans_fit(x, spec["k"], rng, iter_limit=spec["iter_limit"], balanced=True, min_loss_target=1.0,
+                            dist_fn=dist)
+        np.testing.assert_allclose(c, g[f"{tag}_c0"], rtol=1e-5, atol=1e-5)
+        assert np.array_equal(O.nearest(x, c, exact=True), g[f"{tag}_ids"][:, 0])
+
+
+def test_exact_fixture_reference_auctions_are_tie_free(golden):
+    """Every balanced auction of the exact fixtures settles without a tie-rule dependence: on the
+    level-0 scores of the hier case (the reference's first fit, its initial centres = the rows its seed
+    draws), torch's tie rule and the lowest-index rule give the same assignment, which is the blob labels."""
+    g = golden("exact")
+    lab = g["hier_labels"].astype(np.int64)
+    x = _data.exact_rows("hier", lab, g)
+    np.random.seed(42)
+    idx = np.random.choice(len(x), 8, replace=False)
+    s = -O.torch_cdist_batched(x, x[idx])
+    cert = O.auction_tie_certificate(s)
+    assert np.array_equal(cert["torch"], cert["stable"])
+    assert np.array_equal(cert["stable"], lab[:, 0])
