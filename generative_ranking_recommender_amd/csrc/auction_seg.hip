@@ -121,6 +121,13 @@ struct SegAuction {
   uint32_t* lstat;               // [8] list-round verdict counts (RQSID_LIST_STATS=1; null otherwise): ok, no
                                  // list, overflow, leftover round, threshold below the base, too few values,
                                  // too many ties (multi-block)
+  // row-sharded list rounds (rqsid_dauction_*, da_* kernels): dmode[0] = this round slot's mode (kDSweep,
+  // kDList, kDVoid), dmode[1] = 1 in a sweep slot (any_miss points here: the sweep kernels exit otherwise);
+  // each rank's list of worker w is lst[w * dcap ..], walked by dnb blocks per worker
+  uint32_t* dmode;
+  int64_t dcap;
+  int32_t dnb;
+  int32_t dlist_on;              // RQSID_DAUCTION_LIST (default 1): 0 keeps every round a sweep, for A/B
 };
 constexpr int64_t kListMaxJpw = 16384;  // one-block list rounds only while the average jobs per worker per segment is at most this
 constexpr int64_t kListBlockJpw = 8192;  // one wide segment above this many jobs per worker: multi-block list rounds
@@ -1634,6 +1641,7 @@ __global__ void sa_list_layout_kernel(SegAuction a) {
 
 // ---- resolve: per job of the live segments, one block per chunk ----
 __global__ __launch_bounds__(256) void sa_resolve_kernel(SegAuction a, int32_t* __restrict__ out) {
+  if (a.dmode && a.dmode[0] == 2) return;  // a void row-sharded slot changes no job state (kDVoid)
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   if (!(a.flag[ci.s] & kLive)) return;
   resolve_chunk(a, ci, out);
@@ -1747,7 +1755,8 @@ struct Carve {
 };
 
 // workspace layout (also the size query when p == nullptr)
-void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t total_chunks, bool guess) {
+void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t total_chunks, bool guess,
+           bool dlist = false) {
   a.flag = c.take<uint8_t>(S);
   a.eps = c.take<uint16_t>(S);
   a.mm = c.take<uint32_t>(2 * (int64_t)S);
@@ -1760,7 +1769,7 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.hb = c.take<int32_t>(N);
   a.nobid = c.take<uint8_t>(N);
   a.key = c.take<uint32_t>(N);
-  a.hist = c.take<uint32_t>((int64_t)a.n_multi * K * 256);
+  a.hist = c.take<uint32_t>((int64_t)a.n_multi * K * 256 + (dlist ? 64 : 0));  // (+ the list failure count)
   a.sel = c.take<uint32_t>((int64_t)S * K * 4);
   a.eqcnt = c.take<uint32_t>((int64_t)K * total_chunks);
   a.eqtot = c.take<uint32_t>((int64_t)S * K);
@@ -1806,6 +1815,20 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.ldelta = ed ? std::min(128, std::max(1, atoi(ed))) : kListDelta;
   const char* es = getenv("RQSID_LIST_STATS");
   a.lstat = list && es && atoi(es) ? c.take<uint32_t>(8) : nullptr;
+  if (dlist) {  // the row-sharded auction's lists: one rank's share, 8 * (N / K) + 256 entries per worker
+    a.dcap = 8 * (N / K) + 256;
+    a.dnb = (int32_t)std::max<int64_t>(1, (4 * (N / K) + 256 + kMCH - 1) / kMCH);
+    a.lst = c.take<uint2>(a.dcap * K);
+    a.lcnt = c.take<uint32_t>((int64_t)K * kAbovePad);
+    a.lkb = c.take<uint32_t>(K);
+    a.lbad = c.take<uint8_t>(K);
+    a.lany = c.take<uint32_t>(1);
+    a.lsel = c.take<uint32_t>((int64_t)K * 4);
+    a.dmode = c.take<uint32_t>(4);
+    a.any_miss = a.dmode + 1;
+    const char* ed2 = getenv("RQSID_DAUCTION_LIST");
+    a.dlist_on = ed2 ? atoi(ed2) != 0 : 1;
+  }
 }
 
 }  // namespace
@@ -2078,6 +2101,293 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
 namespace {
 constexpr int64_t kDHeader = 512;
 
+// ---- row-sharded list rounds --------------------------------------------------------------------------------
+// The single-process list rounds (sa_list_round_kernel) with the rank's own jobs: a sweep round that starts the
+// list phase appends each worker's values of this rank's jobs with key >= lkb = T - kListDelta (T: the round's
+// threshold, the same on every rank) to the worker's list; the next rounds take their selection, tie ranks and
+// bids from the lists alone.  The collectives are the sweep round's, in the same order, so the host protocol
+// (ShardedAuction.run) does not know which kind of round runs: the list histograms (keys >= lkb) are summed
+// over the ranks like the sweep's, the per-rank counts of values equal to T are all-gathered like the sweep's,
+// and `have` is summed.  Validity is global and decided on every rank from reduced data only: no rank's list
+// overflowed (a count summed with the high-byte histogram), >= jpw + 1 listed values >= lkb over all ranks,
+// T_prev >= lkb and round <= 1000.  When it fails the slot turns void (kDVoid: nothing of the job state
+// changes, the round counter does not advance) and the next slot runs the same round as a sweep, which
+// rebuilds the lists.  Why the lists are exact while they hold: sa_list_round_kernel's argument, per rank
+// (values only fall between rounds except the previous winner's, a worker only wins jobs it bid on, i.e.
+// listed ones).  The ties at T: the first `need` equal values in global job order bid, the ranks' blocks
+// follow each other, so rank r's equal values rank after the lower ranks' (rank_off, from the gather).
+constexpr uint32_t kDSweep = 0, kDList = 1, kDVoid = 2;
+
+__device__ __forceinline__ bool dl_build_round(const SegAuction& a) {  // the next round runs from lists
+  const int next = *a.round_dev + 1;
+  return a.dlist_on && next >= a.lstart && next <= 1000;
+}
+
+// before a list build: empty lists with base key lkb = T - delta
+__global__ __launch_bounds__(256) void da_list_prep_kernel(SegAuction a) {
+  if (a.dmode[0] != kDSweep || !dl_build_round(a) || !(a.flag[0] & kLive)) return;
+  for (int w = blockIdx.x * 256 + threadIdx.x; w < a.K; w += gridDim.x * 256) {
+    a.lcnt[(int64_t)w * kAbovePad] = 0;
+    const uint32_t T = a.sel[(int64_t)w * 4 + 2];
+    a.lkb[w] = T > (uint32_t)a.ldelta ? T - (uint32_t)a.ldelta : 0u;
+  }
+}
+
+// the build: every value of this rank's chunk with key >= lkb, as {local job, raw score}; one global atomic
+// per (block, worker) reserves its range (entries past the capacity are dropped: the next list round fails)
+template <bool VEC>
+__global__ __launch_bounds__(256) void da_list_build_kernel(SegAuction a) {
+  if (a.dmode[0] != kDSweep || !dl_build_round(a)) return;
+  const ChunkInfo ci = chunk_info(a, blockIdx.x);
+  if (!(a.flag[ci.s] & kLive)) return;
+  __shared__ uint32_t cnt[kKG], base[kKG];
+  const int w0 = blockIdx.y * kKG, nw = min(kKG, a.K - w0);
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < kKG) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t kb[kKG];
+#pragma unroll
+  for (int g = 0; g < kKG; ++g) kb[g] = g < nw ? a.lkb[w0 + g] : 0xFFFFFFFFu;
+  ChunkScores cs;
+  load_chunk<VEC>(a, ci, w0, cs);
+  uint32_t mine[kKG] = {};
+#pragma unroll
+  for (int t = 0; t < kJPT; ++t) {
+    const bool live = job_of<VEC>(t) < ci.nj;
+#pragma unroll
+    for (int g = 0; g < kKG; ++g) {
+      const bool in = live && okey(value_bits(w0 + g, cs.v[t][g], cs.hb[t], cs.c[t])) >= kb[g];
+      mine[g] |= (uint32_t)in << t;
+      const uint32_t c = (uint32_t)__popcll(__ballot(in));
+      if (lane == 0 && c) atomicAdd(&cnt[g], c);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < nw) {
+    const uint32_t c = cnt[threadIdx.x];
+    base[threadIdx.x] = c ? atomicAdd(&a.lcnt[(int64_t)(w0 + threadIdx.x) * kAbovePad], c) : 0u;
+    cnt[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  const uint32_t cap = (uint32_t)a.dcap;
+#pragma unroll
+  for (int g = 0; g < kKG; ++g) {
+    if (!mine[g]) continue;
+#pragma unroll
+    for (int t = 0; t < kJPT; ++t) {
+      if (!((mine[g] >> t) & 1u)) continue;
+      const uint32_t pos = base[g] + atomicAdd(&cnt[g], 1u);
+      if (pos < cap)
+        a.lst[(int64_t)(w0 + g) * a.dcap + pos] = make_uint2((uint32_t)(ci.j0 + job_of<VEC>(t)), cs.v[t][g]);
+    }
+  }
+}
+
+// the list passes, a grid of K x dnb blocks (block c of worker w walks the worker's entry chunks c, c + dnb, ..):
+// STEP 0: this round's keys (kept in the entries' upper 16 bits; an overflowed list counts into the failure
+// word) and the high-byte histogram of the keys >= lkb; 1: the low-byte histogram of bin b1; 2: this rank's
+// count of values equal to T; 3: the bids
+template <int STEP>
+__global__ __launch_bounds__(256) void da_list_pass_kernel(SegAuction a) {
+  if (a.dmode[0] != kDList || !(a.flag[0] & kLive)) return;
+  const int w = (int)(blockIdx.x / a.dnb), c0 = (int)(blockIdx.x % a.dnb);
+  const int tid = threadIdx.x;
+  const uint32_t cap = (uint32_t)a.dcap, n_raw = a.lcnt[(int64_t)w * kAbovePad], n = min(n_raw, cap);
+  uint2* const L = a.lst + (int64_t)w * a.dcap;
+  const uint32_t kb = a.lkb[w];
+  const uint32_t stride = (uint32_t)a.dnb * kMCH;
+  if (STEP == 0 && c0 == 0 && tid == 0 && n_raw > cap) atomicAdd(a.hist + (int64_t)a.K * 256, 1u);
+  if (STEP <= 1) {
+    __shared__ uint32_t hst[256];
+    hst[tid] = 0;
+    __syncthreads();
+    const uint32_t b1 = STEP == 1 ? a.sel[(int64_t)w * 4] : 0u;
+    for (uint32_t i0 = (uint32_t)c0 * kMCH; i0 < n; i0 += stride) {
+      const uint32_t i1 = min(n, i0 + (uint32_t)kMCH);
+      for (uint32_t i = i0 + tid; i < i1; i += 256) {
+        if (STEP == 0) {
+          const uint2 e = L[i];
+          const uint32_t k = okey(value_bits(w, (uint16_t)e.y, a.hb[e.x], a.cost[e.x]));
+          L[i].y = (e.y & 0xFFFFu) | (k << 16);
+          if (k >= kb) atomicAdd(&hst[k >> 8], 1u);
+        } else {
+          const uint32_t k = L[i].y >> 16;
+          if (k >= kb && (k >> 8) == b1) atomicAdd(&hst[k & 255u], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    if (hst[tid]) atomicAdd(&a.hist[(int64_t)w * 256 + tid], hst[tid]);
+    return;
+  }
+  const uint32_t T = a.sel[(int64_t)w * 4 + 2];
+  if (STEP == 2) {
+    uint32_t c = 0;
+    for (uint32_t i0 = (uint32_t)c0 * kMCH; i0 < n; i0 += stride) {
+      const uint32_t i1 = min(n, i0 + (uint32_t)kMCH);
+      for (uint32_t i = i0 + tid; i < i1; i += 256) c += (L[i].y >> 16) == T ? 1u : 0u;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+    if ((tid & 63) == 0 && c) atomicAdd(&a.eqtot[w], c);
+    return;
+  }
+  // STEP 3: values above T bid (x - T) + eps; of the values equal to T the first `need` in global job order
+  // (lsel: 0 none of this rank's, 1 all of them, 2 those with job <= J); the retention override; one packed
+  // {bid, ~worker} atomicMax per job as the sweep's bid kernel
+  const uint32_t md = a.lsel[(int64_t)w * 4 + 1], J = a.lsel[(int64_t)w * 4];
+  const uint16_t eps = a.eps[0];
+  const _Float16 epsh = __builtin_bit_cast(_Float16, eps);
+  const _Float16 vT = __builtin_bit_cast(_Float16, okey_inv(T));
+  const bool ret = *a.round_dev < 100;
+  for (uint32_t i0 = (uint32_t)c0 * kMCH; i0 < n; i0 += stride) {
+    const uint32_t i1 = min(n, i0 + (uint32_t)kMCH);
+    for (uint32_t i = i0 + tid; i < i1; i += 256) {
+      const uint2 e = L[i];
+      const uint32_t j = e.x, k = e.y >> 16;
+      uint32_t bid = 0;
+      if (k > T) {
+        const _Float16 x = __builtin_bit_cast(_Float16, okey_inv(k));
+        bid = __builtin_bit_cast(uint16_t, (_Float16)((_Float16)(x - vT) + epsh));
+      } else if (k == T && (md == 1 || (md == 2 && j <= J))) {
+        bid = eps;
+      }
+      if (ret && a.hb[j] == w) bid = eps;  // retention: the previous winner bids eps on its job
+      if (bid) atomicMax(&a.key[j], (bid << 16) | (0xFFFFu - (uint32_t)w));
+    }
+  }
+}
+
+// the selections from the summed list histograms (one wave per worker), and the round's global list verdict
+template <bool LOW>
+__global__ __launch_bounds__(256) void da_list_select_kernel(SegAuction a) {
+  // (the high-byte selection also runs in a slot another wave has just made void: every wave clears its
+  // worker's histogram for the sweep that follows)
+  if (a.dmode[0] != kDList && (LOW || a.dmode[0] != kDVoid)) return;
+  if (!(a.flag[0] & kLive)) return;
+  const int w = (int)(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (w >= a.K) return;
+  const int lane = threadIdx.x & 63;
+  const uint32_t jpw = (uint32_t)(a.n_glob / a.K);
+  uint32_t* h = a.hist + (int64_t)w * 256;
+  uint32_t* sel = a.sel + (int64_t)w * 4;
+  if (!LOW) {
+    uint32_t tot = h[4 * lane] + h[4 * lane + 1] + h[4 * lane + 2] + h[4 * lane + 3];
+    for (int o = 32; o > 0; o >>= 1) tot += (uint32_t)__shfl_xor((int)tot, o);
+    const bool bad = a.dmode[0] != kDList || a.hist[(int64_t)a.K * 256] != 0 || tot < jpw + 1 || sel[2] < a.lkb[w] ||
+                     *a.round_dev > 1000;
+    if (bad) {  // the slot turns void on every rank (each decides from the same reduced data)
+      if (lane == 0) {
+        a.dmode[0] = kDVoid;
+        *a.lany = 0;
+      }
+    } else {
+      uint32_t b, above;
+      wave_select(h, jpw + 1, b, above);
+      if (lane == 0) {
+        sel[0] = b;
+        sel[1] = jpw + 1 - above;
+        sel[3] = above;
+      }
+    }
+  } else {
+    uint32_t b, above;
+    wave_select(h, sel[1], b, above);
+    if (lane == 0) {
+      const uint32_t T = (sel[0] << 8) | b;
+      sel[3] = jpw - (sel[3] + above);
+      sel[2] = T;
+      a.eqtot[w] = 0;
+    }
+  }
+  for (int i = lane; i < 256; i += 64) h[i] = 0;  // ready for the next histogram
+}
+
+// which of this rank's values equal to T bid: need - rank_off of them (in job order); when that is neither
+// none nor all, J = the (need - rank_off)-th smallest job among them by a radix select over the job bytes.
+// One block per worker (most exit at once: the threshold's ties straddle the rank boundary rarely)
+__global__ __launch_bounds__(256) void da_list_rank_kernel(SegAuction a) {
+  if (a.dmode[0] != kDList || !(a.flag[0] & kLive)) return;
+  const int w = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint32_t need = a.sel[(int64_t)w * 4 + 3], off = a.rank_off ? a.rank_off[w] : 0u, loc = a.eqtot[w];
+  const uint32_t nl = need > off ? min(need - off, loc) : 0u;
+  if (tid == 0) a.lsel[(int64_t)w * 4 + 1] = nl == 0 ? 0u : nl == loc ? 1u : 2u;
+  if (nl == 0 || nl == loc) return;
+  __shared__ uint32_t hst[256];
+  __shared__ uint32_t sh[2];
+  const uint32_t T = a.sel[(int64_t)w * 4 + 2];
+  const uint32_t n = min(a.lcnt[(int64_t)w * kAbovePad], (uint32_t)a.dcap);
+  const uint2* const L = a.lst + (int64_t)w * a.dcap;
+  uint32_t J = 0, rank = nl;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    __syncthreads();
+    hst[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += 256) {
+      const uint2 e = L[i];
+      if ((e.y >> 16) == T && (shift == 24 || (e.x >> (shift + 8)) == J)) atomicAdd(&hst[(e.x >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {  // ascending walk: the bin holding the rank-th smallest
+      const uint32_t h0 = hst[4 * tid], h1 = hst[4 * tid + 1], h2 = hst[4 * tid + 2], h3 = hst[4 * tid + 3];
+      const uint32_t own = h0 + h1 + h2 + h3;
+      uint32_t inc = own;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+        if (tid >= o) inc += y;
+      }
+      const unsigned long long m = __ballot(inc >= rank);
+      const int Ln = m ? __ffsll((long long)m) - 1 : 63;
+      if (tid == Ln) {
+        uint32_t acc = inc - own;
+        const uint32_t hv[4] = {h0, h1, h2, h3};
+        int q = 0;
+        for (; q < 3; ++q) {
+          if (acc + hv[q] >= rank) break;
+          acc += hv[q];
+        }
+        sh[0] = (uint32_t)(4 * Ln + q);
+        sh[1] = rank - acc;
+      }
+    }
+    __syncthreads();
+    J = (J << 8) | sh[0];
+    rank = sh[1];
+  }
+  if (tid == 0) a.lsel[(int64_t)w * 4] = J;
+}
+
+// end of a row-sharded round slot (one block): a void slot leaves the round as it was; otherwise the round
+// counts, the auction is done when the summed `have` covers every job, and the next slot lists iff lists exist
+// (built in this sweep slot or held in this list slot) and the next round is in the list range
+__global__ __launch_bounds__(256) void da_round_end_kernel(SegAuction a) {
+  const uint32_t mode = a.dmode[0];
+  const uint32_t next = mode == kDVoid ? kDSweep : (dl_build_round(a) ? kDList : kDSweep);
+  __syncthreads();  // every thread read the round before thread 0 advances it
+  if (threadIdx.x == 0) {
+    if (mode != kDVoid) {
+      *a.round_dev += 1;
+      if (a.flag[0] & kLive) {
+        a.rounds[0] += 1;
+        if ((int64_t)a.have[0] == a.n_glob) a.flag[0] &= ~kLive;
+      }
+    }
+    a.have[0] = 0;
+    a.dmode[0] = next;
+    a.dmode[1] = next == kDSweep ? 1u : 0u;
+    *a.lany = next == kDSweep ? 1u : 0u;
+    a.hist[(int64_t)a.K * 256] = 0;
+  }
+  for (int w = threadIdx.x; w < a.K; w += 256) a.lbad[w] = next == kDSweep ? 1 : 0;
+}
+
+__global__ void da_list_init_kernel(SegAuction a) {  // the first slot sweeps; no lists yet
+  a.dmode[0] = kDSweep;
+  a.dmode[1] = 1;
+  *a.lany = 1;
+  a.hist[(int64_t)a.K * 256] = 0;
+}
+
 __global__ void dauction_tables_kernel(int32_t* seg_off, int32_t* chunk_off, int32_t n, int32_t nch) {
   seg_off[0] = 0;
   seg_off[1] = n;
@@ -2104,7 +2414,7 @@ int dstate(SegAuction& a, const uint16_t* scores, int32_t k, int64_t n_local, in
   a.chunk_off = (const int32_t*)(p + 64);
   a.rounds = (int32_t*)(p + 128);
   Carve c{p + kDHeader};
-  carve(a, c, n_local, k, 1, nch, false);
+  carve(a, c, n_local, k, 1, nch, false, true);
   if (wsb < kDHeader + c.used) return fail(RQSID_E_WORKSPACE, "dauction: workspace too small");
   return RQSID_OK;
 }
@@ -2118,7 +2428,7 @@ int64_t dws(int64_t n_local, int32_t k) {
   SegAuction a{};
   a.n_multi = 1;
   Carve c{nullptr};
-  carve(a, c, n_local, k, 1, cdiv(n_local, kCh), false);
+  carve(a, c, n_local, k, 1, cdiv(n_local, kCh), false, true);
   return kDHeader + c.used;
 }
 }  // namespace
@@ -2135,7 +2445,7 @@ int rqsid_dauction_layout(int64_t n_local, int32_t n_workers, int64_t* offsets) 
   SegAuction a{};
   a.n_multi = 1;
   Carve c{(char*)nullptr + kDHeader};
-  carve(a, c, n_local, n_workers, 1, cdiv(n_local, kCh), false);
+  carve(a, c, n_local, n_workers, 1, cdiv(n_local, kCh), false, true);
   offsets[0] = (int64_t)((char*)a.mm - (char*)nullptr);     // u32 [2]: max key, min key
   offsets[1] = (int64_t)((char*)a.hist - (char*)nullptr);   // u32 [K][256]
   offsets[2] = (int64_t)((char*)a.eqtot - (char*)nullptr);  // u32 [K]
@@ -2155,8 +2465,11 @@ int rqsid_dauction_begin(const uint16_t* scores, int32_t n_workers, int64_t n_lo
                      (int32_t)n_local, (int32_t)a.total_chunks);
   hipLaunchKernelGGL(sa_seg_init_kernel, dim3(1), dim3(256), 0, st, a, (const uint8_t*)nullptr);
   hipLaunchKernelGGL(sa_multi_index_kernel, dim3(1), dim3(1024), 0, st, a);
-  if (fill_async(a.hist, 0, (size_t)n_workers * 256 * 4, st) != hipSuccess)
+  if (fill_async(a.hist, 0, ((size_t)n_workers * 256 + 64) * 4, st) != hipSuccess ||
+      fill_async(a.lcnt, 0, (size_t)n_workers * kAbovePad * 4, st) != hipSuccess ||
+      fill_async(a.lbad, 1, (size_t)n_workers, st) != hipSuccess || fill_async(a.lsel, 0, (size_t)n_workers * 16, st) != hipSuccess)
     return fail(RQSID_E_LAUNCH, "dauction: memset");
+  hipLaunchKernelGGL(da_list_init_kernel, dim3(1), dim3(1), 0, st, a);
   if (n_local > 0) {
     hipLaunchKernelGGL(sa_job_init_kernel, dim3(grid_cap(cdiv(n_local, 256), 8192)), dim3(256), 0, st, a, n_local);
     hipLaunchKernelGGL(sa_fallback_kernel, dim3((unsigned)a.total_chunks), dim3(256), 0, st, a, out_assign);
@@ -2186,10 +2499,14 @@ int rqsid_dauction_hist(const uint16_t* scores, int32_t n_workers, int64_t n_loc
   const dim3 g((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG));
   hipStream_t st = (hipStream_t)stream;
   const bool vec = dvec(scores, n_local);
+  // (each kernel exits at once unless the slot is its kind: sweep, or list)
   if (low && vec) hipLaunchKernelGGL((sa_hist_kernel<1, true>), g, dim3(256), 0, st, a);
   else if (low) hipLaunchKernelGGL((sa_hist_kernel<1, false>), g, dim3(256), 0, st, a);
   else if (vec) hipLaunchKernelGGL((sa_hist_kernel<0, true>), g, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((sa_hist_kernel<0, false>), g, dim3(256), 0, st, a);
+  const dim3 gl((unsigned)((int64_t)n_workers * a.dnb));
+  if (low) hipLaunchKernelGGL((da_list_pass_kernel<1>), gl, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((da_list_pass_kernel<0>), gl, dim3(256), 0, st, a);
   return check_launch("dauction_hist");
 }
 
@@ -2200,8 +2517,14 @@ int rqsid_dauction_select(const uint16_t* scores, int32_t n_workers, int64_t n_l
   int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
   if (rc) return rc;
   const unsigned g = (unsigned)cdiv(n_workers, 4);
-  if (low) hipLaunchKernelGGL((sa_select_kernel<true>), dim3(g), dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL((sa_select_kernel<false>), dim3(g), dim3(256), 0, (hipStream_t)stream, a);
+  hipStream_t st = (hipStream_t)stream;
+  if (low) {
+    hipLaunchKernelGGL((sa_select_kernel<true>), dim3(g), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((da_list_select_kernel<true>), dim3(g), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((sa_select_kernel<false>), dim3(g), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((da_list_select_kernel<false>), dim3(g), dim3(256), 0, st, a);
+  }
   return check_launch("dauction_select");
 }
 
@@ -2218,9 +2541,16 @@ int rqsid_dauction_eqcount(const uint16_t* scores, int32_t n_workers, int64_t n_
     return RQSID_OK;
   }
   const dim3 g((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG));
-  if (dvec(scores, n_local)) hipLaunchKernelGGL((sa_eqcount_kernel<true>), g, dim3(256), 0, st, a);
+  const bool vec = dvec(scores, n_local);
+  if (vec) hipLaunchKernelGGL((sa_eqcount_kernel<true>), g, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((sa_eqcount_kernel<false>), g, dim3(256), 0, st, a);
   hipLaunchKernelGGL(sa_eqscan_kernel, dim3((unsigned)cdiv(n_workers, 4)), dim3(256), 0, st, a);
+  // a sweep slot before the list phase builds the lists from this round's values (T is final here)
+  hipLaunchKernelGGL(da_list_prep_kernel, dim3((unsigned)cdiv(n_workers, 256)), dim3(256), 0, st, a);
+  if (vec) hipLaunchKernelGGL((da_list_build_kernel<true>), g, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((da_list_build_kernel<false>), g, dim3(256), 0, st, a);
+  // a list slot counts its equal values from the lists
+  hipLaunchKernelGGL((da_list_pass_kernel<2>), dim3((unsigned)((int64_t)n_workers * a.dnb)), dim3(256), 0, st, a);
   return check_launch("dauction_eqcount");
 }
 
@@ -2233,8 +2563,11 @@ int rqsid_dauction_bid(const uint16_t* scores, int32_t n_workers, int64_t n_loca
   if (n_local == 0) return RQSID_OK;
   a.rank_off = rank_off;
   const dim3 g((unsigned)a.total_chunks, (unsigned)cdiv(n_workers, kKG));
-  if (dvec(scores, n_local)) hipLaunchKernelGGL((sa_bid_kernel<true>), g, dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL((sa_bid_kernel<false>), g, dim3(256), 0, (hipStream_t)stream, a);
+  hipStream_t st = (hipStream_t)stream;
+  if (dvec(scores, n_local)) hipLaunchKernelGGL((sa_bid_kernel<true>), g, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((sa_bid_kernel<false>), g, dim3(256), 0, st, a);
+  hipLaunchKernelGGL(da_list_rank_kernel, dim3((unsigned)n_workers), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((da_list_pass_kernel<3>), dim3((unsigned)((int64_t)n_workers * a.dnb)), dim3(256), 0, st, a);
   return check_launch("dauction_bid");
 }
 
@@ -2256,7 +2589,7 @@ int rqsid_dauction_end_round(const uint16_t* scores, int32_t n_workers, int64_t 
   SegAuction a;
   int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
   if (rc) return rc;
-  hipLaunchKernelGGL(sa_round_end_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, a, 0);
+  hipLaunchKernelGGL(da_round_end_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("dauction_end_round");
 }
 

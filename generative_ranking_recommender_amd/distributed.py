@@ -259,7 +259,9 @@ class GpuAuctionPasses:
         ops._lib.check(lib.rqsid_dauction_layout(self.n_local, self.k, offs), "rqsid_dauction_layout")
         k = self.k
         self._mm = self.ws[offs[0]:offs[0] + 8].view(torch.int32)
-        self._hist = self.ws[offs[1]:offs[1] + k * 256 * 4].view(torch.int32).view(k, 256)
+        # the K x 256 radix histograms and, after them, the count of ranks whose bid list overflowed (the
+        # row-sharded list rounds, auction_seg.hip da_*): one buffer, one all_reduce
+        self._hist = self.ws[offs[1]:offs[1] + (k * 256 + 1) * 4].view(torch.int32)
         self._eqtot = self.ws[offs[2]:offs[2] + k * 4].view(torch.int32)
         self._have = self.ws[offs[3]:offs[3] + 4].view(torch.int32)
         self._flag = self.ws[offs[4]:offs[4] + 1]
@@ -387,12 +389,20 @@ class ShardedAuction:
                 raise RuntimeError(f"auction: no complete assignment after {max_rounds} rounds")
 
 
+def _force_sharded() -> bool:
+    """RQSID_SHARDED_AUCTION=1: a world-1 group runs the row-sharded protocol too (ShardedAuction over the
+    group's collectives) instead of the single-process auction, so one rank measures what each rank of a
+    larger world runs (tools/train_bench.py --sharded)."""
+    import os
+    return os.environ.get("RQSID_SHARDED_AUCTION", "0") not in ("", "0")
+
+
 def sharded_balanced_assign(x_local: torch.Tensor, centers: torch.Tensor, n_global: int, half: bool = False,
                             group=None) -> torch.Tensor:
     """auction_lap_half(-pairwise_distance(X, C)) with X row-sharded: each rank scores its rows against all
     centres (rqsid_auction_scores) and the ranks run one ShardedAuction.  Returns this rank's worker ids."""
     w = ops.auction_scores(x_local.contiguous(), centers.float().contiguous(), half=half)
-    if dist.get_world_size(group) == 1:
+    if dist.get_world_size(group) == 1 and not _force_sharded():
         # one rank holds every job: the single-process auction of the same scores (identical assignment,
         # see ShardedAuction), which also runs the bid-list rounds the per-round collectives cannot
         a, _ = ops.auction(w)

@@ -236,10 +236,16 @@ int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_
  * (lowest GLOBAL job index at the top-k boundary, lowest worker among equal bids) are those of
  * rqsid_auction_lap_half, so the assignment equals the single-process auction of the whole matrix.
  * rqsid_dauction_layout gives the byte offsets, inside the workspace, of the buffers the caller
- * reduces: [0] u32[2] {max key, min key} (min initialised to 0xFFFFFFFF), [1] u32 [k][256] histogram,
- * [2] u32 [k] eqtot, [3] u32 have, and the state it may poll: [4] u8 flag (bit 0: still bidding; cleared by
- * rqsid_dauction_end_round once the reduced `have` equals n_global, after which every pass is a no-op, so
- * the caller need not read it every round), [5] i32 rounds run.  `offsets` holds 6 entries. */
+ * reduces: [0] u32[2] {max key, min key} (min initialised to 0xFFFFFFFF), [1] u32 [k][256] histogram
+ * followed by one u32 (summed with it: the ranks whose bid list overflowed), [2] u32 [k] eqtot, [3] u32
+ * have, and the state it may poll: [4] u8 flag (bit 0: still bidding; cleared by rqsid_dauction_end_round
+ * once the reduced `have` equals n_global, after which every pass is a no-op, so the caller need not read
+ * it every round), [5] i32 rounds run.  `offsets` holds 6 entries.
+ * Bid lists (RQSID_DAUCTION_LIST=0 turns them off): from round 32 (16 at k >= 1024) a round slot may run
+ * from per-rank lists of each worker's values near its threshold instead of sweeping the scores, with the
+ * same calls and collectives in the same order (the histograms then count listed values).  When the
+ * reduced data show a list did not hold, the slot is void (no job state changes, the round does not
+ * count) and the next slot runs that round as a sweep; the result is the sweep's in every case. */
 int64_t rqsid_dauction_workspace_bytes(int64_t n_local, int32_t n_workers);
 int rqsid_dauction_layout(int64_t n_local, int32_t n_workers, int64_t* offsets);
 int rqsid_dauction_begin(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,

@@ -302,23 +302,38 @@ def _gpu_sharded_auction_worker(rank, world, port, w16, out):
     s, e = shard_bounds(n, rank, world)
     try:
         w = torch.from_numpy(np.ascontiguousarray(w16[:, s:e])).to(DEV)
-        a, rounds = ShardedAuction().run(GpuAuctionPasses(w, n), n, w16.shape[0], max_rounds=1100)
+        a, rounds = ShardedAuction().run(GpuAuctionPasses(w, n), n, w16.shape[0], max_rounds=2500)
         out.put((rank, a.cpu().numpy().astype(np.int64), rounds))
     except Exception as exc:  # report instead of leaving the parent waiting
         out.put((rank, None, repr(exc)))
     dist.destroy_process_group()
 
 
-# per-rank shares of a multiple of 4 jobs take the 8-byte-load passes; 3002 (1501 per rank) the 2-byte ones
-@pytest.mark.parametrize("n,k,levels", [(3000, 16, 7), (640, 64, 1000), (3002, 16, 7)])
-def test_sharded_auction_gpu_passes_two_ranks(n, k, levels):
+# per-rank shares of a multiple of 4 jobs take the 8-byte-load passes; 3002 (1501 per rank) the 2-byte ones;
+# N % K != 0 runs 1002 rounds, so the list phase (from round 32; 16 at K >= 1024) carries most of them
+@pytest.mark.parametrize("dlist", ["1", "0"])
+@pytest.mark.parametrize("n,k,levels", [(3000, 16, 7), (640, 64, 1000), (3002, 16, 7), (40001, 128, 0),
+                                        (24002, 1024, 0)])
+def test_sharded_auction_gpu_passes_two_ranks(n, k, levels, dlist, monkeypatch):
     """Two ranks on one GPU (gloo collectives over device tensors), each running the rqsid_dauction_*
     passes on its row block: the concatenation equals the single-process GPU auction (pinned to the
-    oracle above), ties across the shard boundary included."""
+    oracle above), ties across the shard boundary included, with the row-sharded bid lists (dlist "1":
+    list rounds from per-rank lists, void slots re-run as sweeps) and without them (every round sweeps).
+    levels 0: fp16 distances of unit rows to centres (the training scores), otherwise heavily tied levels."""
     import socket
     import torch.multiprocessing as mp
+    monkeypatch.setenv("RQSID_DAUCTION_LIST", dlist)
     rng = np.random.default_rng(n)
-    w16 = (-rng.integers(1, levels + 1, size=(k, n)).astype(np.float32) * np.float32(0.37)).astype(np.float16)
+    if levels:
+        w16 = (-rng.integers(1, levels + 1, size=(k, n)).astype(np.float32) * np.float32(0.37)).astype(np.float16)
+    else:
+        x = synth.small_mixture(n, m=max(64, k), seed=n)
+        x /= np.linalg.norm(x, axis=1, keepdims=True)
+        c = x[rng.choice(n, k, replace=False)] * np.float32(0.9)
+        d = np.sqrt(np.maximum(((x[:, None, :] - c[None]) ** 2).sum(-1), 0)) if n * k <= 4_000_000 else None
+        if d is None:
+            d = np.sqrt(np.maximum((x ** 2).sum(1)[:, None] + (c ** 2).sum(1)[None] - 2 * x @ c.T, 0))
+        w16 = np.ascontiguousarray((-d.T).astype(np.float16))
     sock = socket.socket()
     sock.bind(("127.0.0.1", 0))
     port = sock.getsockname()[1]

@@ -44,6 +44,10 @@ def main():
     ap.add_argument("--preset", choices=("prod", "xl"), default="prod")
     ap.add_argument("--sharded", action="store_true",
                     help="row-sharded trainer through a world-size-1 RCCL process group")
+    ap.add_argument("--sharded-auction", action="store_true",
+                    help="with --sharded: the balanced fits run the row-sharded auction protocol (rqsid_dauction_*, "
+                         "per-round collectives, row-sharded bid lists) even at world 1 (RQSID_SHARDED_AUCTION=1), "
+                         "i.e. what every rank of a larger world runs")
     ap.add_argument("--out", default="")
     ap.add_argument("--data", choices=("small", "bench"), default="small",
                     help="small: synth.small_mixture (host); bench: bench.make_rows (the encode bench's rows, "
@@ -66,6 +70,9 @@ def main():
     cfg = HierarchicalRQKMeansConfig(layer_clusters=lc, need_clusters=need, embedding_dim=512,
                                      iter_limit=a.iter_limit)
     group = None
+    if a.sharded_auction:
+        import os
+        os.environ["RQSID_SHARDED_AUCTION"] = "1"
     if a.sharded:
         import os
         import torch.distributed as dist
@@ -88,7 +95,9 @@ def main():
     ids = np.stack([r.cpu().numpy() for r in res["cluster_ids"]], 1)
     consistent = bool((model.predict(x, reference_quirks=False) == ids).all())
     line = {"rows": a.rows, "data": a.data, "preset": a.preset, "layer_clusters": lc, "need_clusters": need,
-            "path": "sharded (world 1, RCCL)" if a.sharded else "single process",
+            "path": ("sharded (world 1, RCCL)" + (", row-sharded auction protocol" if a.sharded_auction else ""))
+                    if a.sharded else "single process",
+            "dauction_lists": __import__("os").environ.get("RQSID_DAUCTION_LIST", "1"),
             "mode": "sequential" if a.sequential else "lockstep",
             "total_s": round(total, 2),
             "layers": [m for m in h.marks], "unique_ids": int(len(np.unique(ids, axis=0))),
