@@ -588,8 +588,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic Gaussian mixture (4096 blobs, sigma 0.25) generated on device; " +
-                ("PROD-shaped codebooks fitted on a 1M-row sample (short Lloyd fits, random init)" if args.codebooks == "fitted"
-                 else "PROD-shaped codebooks sampled from residual rows"),
+                (f"{'PROD' if NEED[0] == 128 else 'XL'}-shaped codebooks (need {NEED}) " +
+                 ("fitted on a 1M-row sample (short Lloyd fits, random init)" if args.codebooks == "fitted"
+                  else "sampled from residual rows")),
         "config": {"workload": f"3-level RQ encode, {n} x {D} fp32 rows per GPU, need {NEED}, layer_clusters "
                                f"[{NEED[0]},{N_CAND // 2},{N_CAND // 2}] (BASELINE "
                                + ("configs[2]/[3])" if NEED[0] == 128 else "configs[4] encode shapes)"),

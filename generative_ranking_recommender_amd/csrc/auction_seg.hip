@@ -1824,8 +1824,6 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
     a.lbad = c.take<uint8_t>(K);
     a.lany = c.take<uint32_t>(1);
     a.lsel = c.take<uint32_t>((int64_t)K * 4);
-    a.dmode = c.take<uint32_t>(4);
-    a.any_miss = a.dmode + 1;
     const char* ed2 = getenv("RQSID_DAUCTION_LIST");
     a.dlist_on = ed2 ? atoi(ed2) != 0 : 1;
   }
@@ -2381,6 +2379,16 @@ __global__ __launch_bounds__(256) void da_round_end_kernel(SegAuction a) {
   for (int w = threadIdx.x; w < a.K; w += 256) a.lbad[w] = next == kDSweep ? 1 : 0;
 }
 
+// start of a list-only slot (the caller launched no sweep kernel for it): when the slot is a sweep, it turns void
+// (nothing changes; the round runs as a sweep in the first full slot after the caller's next poll)
+__global__ void da_slot_list_only_kernel(SegAuction a) {
+  if (a.dmode[0] == kDSweep) {
+    a.dmode[0] = kDVoid;
+    a.dmode[1] = 0;
+    *a.lany = 0;
+  }
+}
+
 __global__ void da_list_init_kernel(SegAuction a) {  // the first slot sweeps; no lists yet
   a.dmode[0] = kDSweep;
   a.dmode[1] = 1;
@@ -2413,6 +2421,8 @@ int dstate(SegAuction& a, const uint16_t* scores, int32_t k, int64_t n_local, in
   a.seg_off = (const int32_t*)p;
   a.chunk_off = (const int32_t*)(p + 64);
   a.rounds = (int32_t*)(p + 128);
+  a.dmode = (uint32_t*)(p + 192);  // [0] slot mode (the caller may poll it), [1] sweep-slot flag
+  a.any_miss = a.dmode + 1;        // (the sweep kernels exit unless it is set)
   Carve c{p + kDHeader};
   carve(a, c, n_local, k, 1, nch, false, true);
   if (wsb < kDHeader + c.used) return fail(RQSID_E_WORKSPACE, "dauction: workspace too small");
@@ -2591,6 +2601,38 @@ int rqsid_dauction_end_round(const uint16_t* scores, int32_t n_workers, int64_t 
   if (rc) return rc;
   hipLaunchKernelGGL(da_round_end_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("dauction_end_round");
+}
+
+// the list kernels of one pass alone, for list-only slots (the sweep kernels of hist / eqcount / bid are not
+// launched: at K = 2560 over 6.25M jobs each such launch costs ~0.2 ms of dispatch even when every block exits):
+// step -1 starts the slot (a sweep slot turns void), 0 / 1 the histograms, 2 the equal-value counts, 3 the
+// tie ranks and bids (rank_off as for rqsid_dauction_bid)
+int rqsid_dauction_list_pass(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global, int32_t step,
+                             const uint32_t* rank_off, void* workspace, int64_t workspace_bytes, void* stream) {
+  SegAuction a;
+  int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
+  if (rc) return rc;
+  if (step < -1 || step > 3) return fail(RQSID_E_ARG, "dauction_list_pass: step %d", step);
+  hipStream_t st = (hipStream_t)stream;
+  if (step == -1) {
+    hipLaunchKernelGGL(da_slot_list_only_kernel, dim3(1), dim3(1), 0, st, a);
+    return check_launch("dauction_list_pass");
+  }
+  if (n_local == 0) {
+    if (step == 2 && fill_async(a.eqtot, 0, (size_t)n_workers * 4, st) != hipSuccess)
+      return fail(RQSID_E_LAUNCH, "dauction: memset");
+    return RQSID_OK;
+  }
+  const dim3 gl((unsigned)((int64_t)n_workers * a.dnb));
+  a.rank_off = rank_off;
+  if (step == 0) hipLaunchKernelGGL((da_list_pass_kernel<0>), gl, dim3(256), 0, st, a);
+  else if (step == 1) hipLaunchKernelGGL((da_list_pass_kernel<1>), gl, dim3(256), 0, st, a);
+  else if (step == 2) hipLaunchKernelGGL((da_list_pass_kernel<2>), gl, dim3(256), 0, st, a);
+  else {
+    hipLaunchKernelGGL(da_list_rank_kernel, dim3((unsigned)n_workers), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((da_list_pass_kernel<3>), gl, dim3(256), 0, st, a);
+  }
+  return check_launch("dauction_list_pass");
 }
 
 }  // extern "C"

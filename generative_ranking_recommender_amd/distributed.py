@@ -267,6 +267,8 @@ class GpuAuctionPasses:
         self._flag = self.ws[offs[4]:offs[4] + 1]
         self._rounds = self.ws[offs[5]:offs[5] + 4].view(torch.int32)
         self.out = torch.full((max(self.n_local, 1),), -1, dtype=torch.int32, device=self.w.device)
+        self._mode = self.ws[192:196].view(torch.int32)  # the coming slot's mode (include/rqsid.h)
+        self.list_only = False  # set by the driver per slot: launch the list kernels alone
 
     def _args(self):
         return (ops._ptr(self.w) if self.n_local else None, self.k, self.n_local, self.n_global)
@@ -283,7 +285,16 @@ class GpuAuctionPasses:
         self._mm.copy_(torch.tensor([mx, mn], dtype=torch.int64).to(torch.int32))
         ops._lib.check(self.lib.rqsid_dauction_eps(*self._args(), *self._tail()), "rqsid_dauction_eps")
 
+    def _list_pass(self, step: int, rank_off=None) -> None:
+        ops._lib.check(self.lib.rqsid_dauction_list_pass(*self._args(), int(step), ops._ptr(rank_off), *self._tail()),
+                       "rqsid_dauction_list_pass")
+
     def hist(self, low: int) -> torch.Tensor:
+        if self.list_only:
+            if not low:
+                self._list_pass(-1)
+            self._list_pass(int(low))
+            return self._hist
         ops._lib.check(self.lib.rqsid_dauction_hist(*self._args(), int(low), *self._tail()), "rqsid_dauction_hist")
         return self._hist
 
@@ -292,11 +303,17 @@ class GpuAuctionPasses:
                        "rqsid_dauction_select")
 
     def eqcount(self) -> torch.Tensor:
+        if self.list_only:
+            self._list_pass(2)
+            return self._eqtot
         ops._lib.check(self.lib.rqsid_dauction_eqcount(*self._args(), *self._tail()), "rqsid_dauction_eqcount")
         return self._eqtot
 
     def bid(self, rank_off: torch.Tensor) -> None:
         ro = rank_off.to(torch.int32).to(self.w.device).contiguous()
+        if self.list_only:
+            self._list_pass(3, ro)
+            return
         ops._lib.check(self.lib.rqsid_dauction_bid(*self._args(), ops._ptr(ro), *self._tail()), "rqsid_dauction_bid")
 
     def resolve(self) -> torch.Tensor:
@@ -310,6 +327,11 @@ class GpuAuctionPasses:
     def live(self) -> bool:
         """Still bidding (host sync): end_round clears it once the reduced `have` covers every job."""
         return bool(int(self._flag.item()) & 1)
+
+    def lists_hold(self) -> bool:
+        """The coming slot runs from the bid lists (host sync; the same on every rank: it is decided from
+        reduced data only)."""
+        return int(self._mode.item()) == 1
 
     def rounds_run(self) -> int:
         return int(self._rounds.item())
@@ -327,7 +349,9 @@ class ShardedAuction:
     identical thresholds and the same stop decision, and the assignment equals the single-process auction
     of the whole matrix (same fp16 operations, same tie rule).  The stop decision is taken on the device
     (end_round clears the live flag; later passes are no-ops), so the host reads it once per ``poll``
-    rounds instead of synchronising every round."""
+    rounds instead of synchronising every round.  From round 32 (16 at K >= 1024) the GPU passes run
+    rounds from per-rank bid lists (auction_seg.hip da_*, same collectives); at each poll the host also
+    reads whether the lists hold and then launches list-only slots (rqsid_dauction_list_pass)."""
 
     poll = 8
 
@@ -366,6 +390,7 @@ class ShardedAuction:
         self._all_reduce(mn, dist.ReduceOp.MIN)
         passes.set_minmax(int(mx.item()), int(mn.item()))
         issued = 0
+        lists = getattr(passes, "lists_hold", None)
         while True:
             for low in (0, 1):
                 h = passes.hist(low)
@@ -387,6 +412,10 @@ class ShardedAuction:
                 return passes.result(), passes.rounds_run()
             if max_rounds and issued >= max_rounds:
                 raise RuntimeError(f"auction: no complete assignment after {max_rounds} rounds")
+            if lists is not None:
+                # the next slots launch the list kernels alone while the lists hold (a slot that meets a sweep
+                # round is void and the poll after it returns to full slots); every rank reads the same mode
+                passes.list_only = lists()
 
 
 def _force_sharded() -> bool:

@@ -247,6 +247,14 @@ int rqsid_seg_auction_lap_half(const uint16_t* scores, int32_t n_workers, int32_
  * reduced data show a list did not hold, the slot is void (no job state changes, the round does not
  * count) and the next slot runs that round as a sweep; the result is the sweep's in every case. */
 int64_t rqsid_dauction_workspace_bytes(int64_t n_local, int32_t n_workers);
+/* List-only round slots: workspace bytes [192, 196) hold the mode of the coming slot (u32: 0 sweep, 1 list,
+ * 2 void), identical on every rank.  While it reads 1 the caller may run a slot as list_pass(-1),
+ * list_pass(0), sum, select(0), list_pass(1), sum, select(1), list_pass(2), gather, list_pass(3, rank_off),
+ * resolve, sum, end_round: the same collectives without launching the sweep kernels; a list-only slot that
+ * meets a sweep round is void (nothing changes) and the caller returns to full slots at its next poll. */
+int rqsid_dauction_list_pass(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
+                             int32_t step, const uint32_t* rank_off, void* workspace, int64_t workspace_bytes,
+                             void* stream);
 int rqsid_dauction_layout(int64_t n_local, int32_t n_workers, int64_t* offsets);
 int rqsid_dauction_begin(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
                          int32_t* out_assign, void* workspace, int64_t workspace_bytes, void* stream);
