@@ -128,6 +128,10 @@ struct SegAuction {
   int64_t dcap;
   int32_t dnb;
   int32_t dlist_on;              // RQSID_DAUCTION_LIST (default 1): 0 keeps every round a sweep, for A/B
+  // one-segment auctions (single process): {blocks arrived << 32 | jobs with a bidder} of the round's resolve;
+  // the last block to arrive ends the round (sa_round_end_kernel's work, one launch fewer per round)
+  unsigned long long* rdone;
+  int32_t rcount;                // end-of-round: add the live count for the host's poll (a block's last round)
 };
 constexpr int64_t kListMaxJpw = 16384;  // one-block list rounds only while the average jobs per worker per segment is at most this
 constexpr int64_t kListBlockJpw = 8192;  // one wide segment above this many jobs per worker: multi-block list rounds
@@ -1069,7 +1073,24 @@ __device__ __forceinline__ void resolve_chunk(const SegAuction& a, const ChunkIn
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t tot = wc[0] + wc[1] + wc[2] + wc[3];
-    if (tot) atomicAdd(&a.have[ci.s], tot);
+    if (a.rdone) {
+      // one 64-bit atomic carries both the arrival and the count, so the last block to arrive sees every
+      // other block's count in the value it gets back (no fence between two atomics needed)
+      const unsigned long long old = atomicAdd(a.rdone, (1ull << 32) | tot);
+      if ((old >> 32) == (unsigned long long)(gridDim.x - 1)) {
+        const uint32_t have = (uint32_t)old + tot;
+        *a.round_dev += 1;
+        if (a.any_miss) *a.any_miss = 0;
+        if (a.lany) *a.lany = 0;
+        a.rounds[0] += 1;
+        const bool live = (int64_t)have != (int64_t)(a.seg_off[1] - a.seg_off[0]);
+        if (!live) a.flag[0] &= ~kLive;
+        *a.rdone = 0;
+        if (a.rcount && live) atomicAdd(a.live_count, 1u);
+      }
+    } else if (tot) {
+      atomicAdd(&a.have[ci.s], tot);
+    }
   }
 }
 
@@ -1813,6 +1834,7 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.lstart = ls ? std::max(1, atoi(ls)) : K >= kListWideK ? kListStartWide : kListStart;
   const char* ed = getenv("RQSID_LIST_DELTA");
   a.ldelta = ed ? std::min(128, std::max(1, atoi(ed))) : kListDelta;
+  a.rdone = guess && S == 1 && a.n_multi == 1 ? c.take<unsigned long long>(1) : nullptr;
   const char* es = getenv("RQSID_LIST_STATS");
   a.lstat = list && es && atoi(es) ? c.take<uint32_t>(8) : nullptr;
   if (dlist) {  // the row-sharded auction's lists: one rank's share, 8 * (N / K) + 256 entries per worker
@@ -1895,7 +1917,8 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     return fail(RQSID_E_LAUNCH, "seg_auction: pinned readback buffer");
   }
   int rc = RQSID_OK;
-  if (fill_async(a.live_count, 0, 16, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "seg_auction: memset");
+  if (fill_async(a.live_count, 0, 16, st) != hipSuccess || (a.rdone && fill_async(a.rdone, 0, 8, st) != hipSuccess))
+    return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   hipLaunchKernelGGL(sa_seg_init_kernel, dim3(gs), dim3(256), 0, st, a, active);
   hipLaunchKernelGGL(sa_multi_index_kernel, dim3(1), dim3(1024), 0, st, a);
   if ((rc = check_launch("seg_auction_init")) ||
@@ -1965,9 +1988,11 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     } else if (a.lst) {
       hipLaunchKernelGGL(sa_list_round_kernel, dim3((unsigned)(n_multi * a.K)), dim3(kLT), 0, q, a);
     }
+    SegAuction ar = a;
+    ar.rcount = count ? 1 : 0;
     if (list_only) {
-      hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, q, a, out_assign);
-      hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
+      hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, q, ar, out_assign);
+      if (!a.rdone) hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
       return;
     }
     if (n_multi > 0) {
@@ -1991,8 +2016,8 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     if (any_single) hipLaunchKernelGGL(sa_small_select_kernel, gcw, dim3(256), 0, q, a);
     if (vec) hipLaunchKernelGGL((sa_bid_kernel<true>), gcw, dim3(256), 0, q, a);
     else hipLaunchKernelGGL((sa_bid_kernel<false>), gcw, dim3(256), 0, q, a);
-    hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, q, a, out_assign);
-    hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
+    hipLaunchKernelGGL(sa_resolve_kernel, gc, dim3(256), 0, q, ar, out_assign);
+    if (!a.rdone) hipLaunchKernelGGL(sa_round_end_kernel, dim3(gs), dim3(256), 0, q, a, (int)count);
   };
   // capture blocks on a private stream (the caller's may be the null stream, which cannot capture)
   auto capture = [&](bool lean, bool list_only = false) {
