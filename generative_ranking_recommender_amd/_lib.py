@@ -66,6 +66,7 @@ SIGNATURES = {
     "rqsid_seg_auction_workspace_bytes": (c_i64, [c_i64, c_i32, c_i32, c_i64, c_i32]),
     "rqsid_seg_auction_lap_half": (c_i32, [c_vp, c_i32, c_i32, c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_i32, c_vp,
                                            c_vp, c_vp, c_i64, c_vp]),
+    "rqsid_pairwise_cosine": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp]),
     "rqsid_dauction_workspace_bytes": (c_i64, [c_i64, c_i32]),
     "rqsid_dauction_layout": (c_i32, [c_i64, c_i32, c_vp]),
     "rqsid_dauction_begin": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),

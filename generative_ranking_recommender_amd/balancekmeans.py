@@ -3,7 +3,7 @@
 kernels of ``librqsid.so``:
 
 * distances + argmin  -> ``rqsid_assign`` (exact argmin; the reference's fp32 ``torch.cdist``
-  + ``torch.argmin``, :489-534, 576-603)
+  + ``torch.argmin``, :489-534, 576-603); ``distance='cosine'`` -> ``rqsid_pairwise_cosine`` (:625-655)
 * balanced assignment -> ``rqsid_auction_scores`` + ``rqsid_auction_lap_half`` (:12-140)
 * centroid update     -> ``rqsid_centroid_accumulate/finalize`` (fp64 sums, :315-324)
 
@@ -64,6 +64,13 @@ def pairwise_distance_half(data1, data2, device=None, batch_size: int = 20000) -
     clamped at 1e-5."""
     dev = _device(device)
     return (-ops.auction_scores(_to_dev(data1, dev), _to_dev(data2, dev), half=True)).t().contiguous()
+
+
+def pairwise_cosine(data1, data2, device=None, batch_size: int = 1000) -> torch.Tensor:
+    """balancekmeans/__init__.py:625-655: fp32 [N, K] cosine distances 1 - x.c / (|x||c|)
+    (``rqsid_pairwise_cosine``; ``batch_size`` is accepted for signature compatibility)."""
+    dev = _device(device)
+    return ops.pairwise_cosine(_to_dev(data1, dev), _to_dev(data2, dev))
 
 
 def auction_lap_half(job_and_worker_to_score: torch.Tensor, return_token_to_worker: bool = True) -> torch.Tensor:
@@ -133,11 +140,21 @@ class KMeans:
         return X[torch.from_numpy(np.asarray(indices)).to(X.device)].clone()
 
     def _check_distance(self, distance):
-        if distance != "euclidean":
-            raise NotImplementedError(f"distance={distance!r}: only 'euclidean' is on the semantic-ID path")
+        """'euclidean' (the semantic-ID path) and 'cosine' (:279-280, 625-655); 'soft_dtw' needs the
+        reference's numba-CUDA SoftDTW and stays out of scope."""
+        if distance not in ("euclidean", "cosine"):
+            raise NotImplementedError(f"distance={distance!r}: 'euclidean' and 'cosine' are supported")
+        self._distance = distance
 
     def _assign(self, X: torch.Tensor, half: bool) -> torch.Tensor:
         self._scores, self._x, self._half = None, X, half
+        if getattr(self, "_distance", "euclidean") == "cosine":
+            # pairwise_cosine for the assignment whatever `half` says (:279-280); argmin = first index
+            if self.balanced:
+                a, rounds = ops.auction(ops.pairwise_cosine(X, self.cluster_centers, scores=True))
+                self.last_auction_rounds.append(rounds)
+                return a
+            return torch.argmin(ops.pairwise_cosine(X, self.cluster_centers), dim=1)
         if self.balanced:
             w = ops.auction_scores(X, self.cluster_centers, half=half)
             a, rounds = ops.auction(w)
@@ -148,7 +165,7 @@ class KMeans:
         return ops.nearest(X, ops.prepare_centers(self.cluster_centers))
 
     def _emit(self, iteration: int, prev: torch.Tensor, a: torch.Tensor, loss=None, target=None) -> None:
-        if self.trace is not None:
+        if self.trace is not None and getattr(self, "_distance", "euclidean") == "euclidean":
             self.trace({"kind": "fit", "owner": self._owner, "x": self._x, "half": self._half,
                         "iteration": iteration, "centers_in": prev.clone(), "scores": self._scores,
                         "assign": a.clone(), "centers_out": self.cluster_centers.clone(), "loss": loss,
@@ -185,7 +202,11 @@ class KMeans:
                 self.cluster_centers = self.initialize(X)
             a = self._assign(X, half)
             prev = self._update(X, a)
-            counts = torch.bincount(_loss_assign(X, self.cluster_centers, half), minlength=self.n_clusters)
+            if distance == "cosine":
+                near = torch.argmin(ops.pairwise_cosine(X, self.cluster_centers), dim=1)
+            else:
+                near = _loss_assign(X, self.cluster_centers, half)
+            counts = torch.bincount(near, minlength=self.n_clusters)
             over = counts - target_nodes_num
             cur_loss = float(over[over > 0].sum().item()) if (over > 0).any() else 0
             self._emit(iteration, prev, a, cur_loss, target_nodes_num)
@@ -232,6 +253,10 @@ class KMeans:
         if X.dim() == 1:
             X = X.unsqueeze(0)
         c = self.cluster_centers.float().to(self.device).contiguous()
+        if distance == "cosine":
+            d = ops.pairwise_cosine(X, c)
+            ids = (auction_lap_full(-d) if balanced else torch.argmin(d, dim=1)).long().cpu()
+            return (ids, d) if return_distances else ids
         if balanced:
             d = ops.pairwise_distance(X, c)
             ids = auction_lap_full(-d).cpu()

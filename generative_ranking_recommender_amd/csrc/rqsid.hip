@@ -438,10 +438,18 @@ __global__ __launch_bounds__(256) void pairwise_distance_kernel(const float* __r
     for (int j = 0; j < 4; ++j) {
       const int cc = c0 + tx + 16 * j;
       if (cc >= k) continue;
-      const float d2 = MODE == 2 ? (float)(_Float16)((-2.f * acc[i][j] + xq[i]) + cq[j])
-                                 : (-2.f * acc[i][j] + xq[i]) + cq[j];
-      const float d = sqrtf(fmaxf(d2, 0.f));
-      if (MODE == 0) {
+      float d;
+      if (MODE == 3) {  // cosine distance 1 - x.c / (|x| |c|) (pairwise_cosine, :625-655)
+        d = 1.f - acc[i][j] / (sqrtf(xq[i]) * sqrtf(cq[j]));
+      } else {
+        const float d2 = MODE == 2 ? (float)(_Float16)((-2.f * acc[i][j] + xq[i]) + cq[j])
+                                   : (-2.f * acc[i][j] + xq[i]) + cq[j];
+        d = sqrtf(fmaxf(d2, 0.f));
+      }
+      if (MODE == 3) {
+        if (out) out[rr * k + cc] = d;
+        if (out16) out16[(int64_t)cc * n_s + (rr - seg_base)] = __builtin_bit_cast(uint16_t, (_Float16)(-d));
+      } else if (MODE == 0) {
         out[rr * k + cc] = d;
       } else if (MODE == 1) {
         out16[(int64_t)cc * n_s + (rr - seg_base)] = __builtin_bit_cast(uint16_t, (_Float16)(-d));
@@ -680,6 +688,16 @@ int rqsid_pairwise_distance(const float* x, int64_t n, int32_t dim, const float*
   hipLaunchKernelGGL(pairwise_distance_kernel<0>, dim3((unsigned)cdiv(n, kPdTile), (unsigned)cdiv(k, kPdTile)),
                      dim3(256), 0, (hipStream_t)stream, x, n, dim, centers, k, out, (uint16_t*)nullptr);
   return check_launch("pairwise_distance");
+}
+
+int rqsid_pairwise_cosine(const float* x, int64_t n, int32_t dim, const float* centers, int32_t k, float* out,
+                          uint16_t* out_wj, void* stream) {
+  if (!x || !centers || (!out && !out_wj) || n < 0 || k <= 0 || dim <= 0 || dim % 32)
+    return fail(RQSID_E_ARG, "pairwise_cosine: bad arguments");
+  if (n == 0) return RQSID_OK;
+  hipLaunchKernelGGL(pairwise_distance_kernel<3>, dim3((unsigned)cdiv(n, kPdTile), (unsigned)cdiv(k, kPdTile)),
+                     dim3(256), 0, (hipStream_t)stream, x, n, dim, centers, k, out, out_wj);
+  return check_launch("pairwise_cosine");
 }
 
 int rqsid_auction_scores(const float* x, int64_t n, int32_t dim, const float* centers, int32_t k, int32_t half,

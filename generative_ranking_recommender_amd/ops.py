@@ -323,6 +323,23 @@ def pairwise_distance(x: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def pairwise_cosine(x: torch.Tensor, c: torch.Tensor, scores: bool = False) -> torch.Tensor:
+    """Cosine distances 1 - x.c / (|x||c|): fp32 [N, K], or with ``scores`` the auction's worker-major fp16
+    [K][N] = -distance (include/rqsid.h rqsid_pairwise_cosine)."""
+    c = c.float().contiguous()
+    _require_device(x, c)
+    n, d = x.shape
+    if scores:
+        out = torch.empty((c.shape[0], n), dtype=torch.float16, device=x.device)
+        _lib.check(lib().rqsid_pairwise_cosine(_ptr(x), n, d, _ptr(c), c.shape[0], None, _ptr(out), _stream()),
+                   "rqsid_pairwise_cosine")
+        return out
+    out = torch.empty((n, c.shape[0]), dtype=torch.float32, device=x.device)
+    _lib.check(lib().rqsid_pairwise_cosine(_ptr(x), n, d, _ptr(c), c.shape[0], _ptr(out), None, _stream()),
+               "rqsid_pairwise_cosine")
+    return out
+
+
 def auction_scores(x: torch.Tensor, c: torch.Tensor, half: bool = False) -> torch.Tensor:
     """Worker-major fp16 scores W[k][n] = -distance (the auction's input), see include/rqsid.h."""
     c = c.float().contiguous()

@@ -165,6 +165,14 @@ int rqsid_match_to_candidates(const uint8_t* match, int32_t groups, int32_t n_ca
 int rqsid_pairwise_distance(const float* x, int64_t n, int32_t dim, const float* centers,
                             int32_t k, float* out, void* stream);
 
+/* Cosine distances 1 - x.c / (|x| |c|) of pairwise_cosine (balancekmeans/__init__.py:625-655, the
+ * distance='cosine' option of KMeans.fit / fit_by_min_loss / predict, :279-280, 511-512): fp32 [n][k] into
+ * `out` and / or the auction's worker-major fp16 scores -distance [k][n] into `out_wj` (either may be NULL).
+ * fp32 sums in the kernel's order (the reference normalises the operands first, then multiplies: the
+ * results agree to a few fp32 ulps of 1). */
+int rqsid_pairwise_cosine(const float* x, int64_t n, int32_t dim, const float* centers, int32_t k, float* out,
+                          uint16_t* out_wj, void* stream);
+
 /* Auction score matrix: out_wj[k][n] = fp16(-||x_i - c_j||) (fp32 distances, half = 0) or
  * -max(fp16 distance of the fp16-rounded operands, 1e-5) (half != 0), worker-major: the input of
  * auction_lap_half(-pairwise_distance_{full,half}(X, C)), balancekmeans/__init__.py:29-43,

@@ -38,6 +38,16 @@ def cdist_f32(x: np.ndarray, c: np.ndarray) -> np.ndarray:
     return np.sqrt(np.maximum(d2, F32(0.0)), dtype=F32)
 
 
+def pairwise_cosine(x: np.ndarray, c: np.ndarray) -> np.ndarray:
+    """balancekmeans/__init__.py:625-655 pairwise_cosine: both operands divided by their fp32 row norms,
+    then 1 - the fp32 matrix product (the distance='cosine' option of KMeans, :279-280, 511-512)."""
+    x = x.astype(F32, copy=False)
+    c = c.astype(F32, copy=False)
+    xn = (x / np.sqrt((x.astype(np.float64) ** 2).sum(1, keepdims=True)).astype(F32)).astype(F32)
+    cn = (c / np.sqrt((c.astype(np.float64) ** 2).sum(1, keepdims=True)).astype(F32)).astype(F32)
+    return (F32(1.0) - xn @ cn.T).astype(F32)
+
+
 def torch_cdist_batched(x: np.ndarray, c: np.ndarray, batch_size: int = 10000) -> np.ndarray:
     """pairwise_distance_full (balancekmeans/__init__.py:576-603) itself: torch.cdist on the CPU over
     batches of 10000 rows (the third-party arithmetic the reference calls; its summation order is that

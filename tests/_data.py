@@ -148,3 +148,15 @@ def exact_rows(tag, labels, g=None):
     if g is not None:
         checked(x, g[f"{tag}_x_sha"])
     return x
+
+
+def cosine_inputs(g=None):
+    """KMeans(distance='cosine') fixture (make_golden.py g_cosine): 512 rows of 8 well separated directions
+    at varied norms, and 40 centre rows of the same mixture."""
+    x = synth.small_mixture(512, m=8, sigma=0.2, seed=91)
+    x *= np.random.default_rng(92).uniform(0.5, 3.0, size=(512, 1)).astype(np.float32)
+    x = x.astype(np.float32)
+    c = synth.small_mixture(40, m=8, sigma=0.2, seed=93)
+    if g is not None:
+        checked(x, g["x_sha"])
+    return x, c

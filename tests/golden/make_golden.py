@@ -525,6 +525,30 @@ def g_exact():
     save("exact", **out)
 
 
+# --- G-cosine: KMeans(distance='cosine') (:279-280, 511-512, pairwise_cosine :625-655) ------------------
+def g_cosine():
+    """pairwise_cosine on fixed rows; KMeans(balanced=True).fit / fit_by_min_loss and the unbalanced fit with
+    distance='cosine' (seeded); predict(distance='cosine')."""
+    from tests import _data
+    x, c = _data.cosine_inputs()
+    d = ref_bk.pairwise_cosine(torch.from_numpy(x), torch.from_numpy(c))
+    out = {"x_sha": np.array(synth.sha256(x)), "d": d.numpy()}
+    seed_all(31)
+    km = ref_bk.KMeans(n_clusters=8, balanced=True)
+    a = km.fit(torch.from_numpy(x), distance="cosine", iter_limit=4, tqdm_flag=False)
+    out.update(fit_bal_assign=a.numpy().astype(np.int64), fit_bal_centers=km.cluster_centers.numpy())
+    out["pred"] = km.predict(torch.from_numpy(x), distance="cosine").numpy().astype(np.int64)
+    seed_all(32)
+    km2 = ref_bk.KMeans(n_clusters=8, balanced=False)
+    a2 = km2.fit(torch.from_numpy(x), distance="cosine", iter_limit=3, tqdm_flag=False)
+    out.update(fit_unbal_assign=a2.numpy().astype(np.int64), fit_unbal_centers=km2.cluster_centers.numpy())
+    seed_all(33)
+    km3 = ref_bk.KMeans(n_clusters=8, balanced=True)
+    km3.fit_by_min_loss(torch.from_numpy(x), target_nodes_num=64, distance="cosine", iter_limit=4, tqdm_flag=False)
+    out["fbml_centers"] = km3.cluster_centers.numpy()
+    save("cosine", **out)
+
+
 # --- G-csv: loader skip rules (simplified :38-76) ----------------------------
 def g_csv():
     rows = [["a", "1", "2", "3", "4"], ["b"], ["c", "1", "x", "3", "4"], ["d", "1", "2", "3"],
@@ -546,6 +570,6 @@ def g_csv():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["assign", "residual", "update", "auction", "fit", "simplified",
-                             "hierarchical", "encode_prod", "csv", "dist_half", "trainer", "match", "config0", "exact"]
+                             "hierarchical", "encode_prod", "csv", "dist_half", "trainer", "match", "config0", "exact", "cosine"]
     for w in which:
         globals()[f"g_{w}"]()

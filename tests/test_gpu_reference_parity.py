@@ -453,3 +453,31 @@ def test_semantic_id_trainer_files_match_reference(golden, tmp_path):
     assert (tmp_path / "models" / "semantic_id" / "config.json").exists()
     report("semantic_id_trainer", agree_per_level=(ids == g["ids"]).mean(0),
            unique_ref=ref_stats["unique_semantic_ids"], unique_gpu=stats["unique_semantic_ids"])
+
+
+def test_cosine_distance_kmeans_against_reference(golden):
+    """KMeans(distance='cosine') (balancekmeans/__init__.py:279-280, 511-512) on rqsid_pairwise_cosine
+    against the reference's outputs (tests/golden/cosine.npz): the fp32 distances within a few ulps of 1
+    (the reference normalises the operands first), the balanced and unbalanced fits and predict on
+    well-separated directions identical, the min-loss centres within 1e-4."""
+    g = golden("cosine")
+    x, c = _data.cosine_inputs(g)
+    d = bk.pairwise_cosine(torch.from_numpy(x), torch.from_numpy(c), device=DEV).cpu().numpy()
+    np.testing.assert_allclose(d, g["d"], rtol=0, atol=3e-6)
+    seeded(31)
+    km = bk.KMeans(n_clusters=8, device=DEV, balanced=True)
+    a = km.fit(torch.from_numpy(x), distance="cosine", iter_limit=4, tqdm_flag=False).numpy()
+    assert np.array_equal(a, g["fit_bal_assign"])
+    np.testing.assert_allclose(km.cluster_centers.cpu().numpy(), g["fit_bal_centers"], rtol=1e-4, atol=1e-4)
+    assert np.array_equal(km.predict(torch.from_numpy(x), distance="cosine").numpy(), g["pred"])
+    seeded(32)
+    km2 = bk.KMeans(n_clusters=8, device=DEV, balanced=False)
+    a2 = km2.fit(torch.from_numpy(x), distance="cosine", iter_limit=3, tqdm_flag=False).numpy()
+    assert np.array_equal(a2, g["fit_unbal_assign"])
+    np.testing.assert_allclose(km2.cluster_centers.cpu().numpy(), g["fit_unbal_centers"], rtol=1e-4, atol=1e-4)
+    seeded(33)
+    km3 = bk.KMeans(n_clusters=8, device=DEV, balanced=True)
+    km3.fit_by_min_loss(torch.from_numpy(x), target_nodes_num=64, distance="cosine", iter_limit=4, tqdm_flag=False)
+    np.testing.assert_allclose(km3.cluster_centers.cpu().numpy(), g["fbml_centers"], rtol=1e-4, atol=1e-4)
+    with pytest.raises(NotImplementedError):
+        bk.KMeans(n_clusters=8, device=DEV).fit(torch.from_numpy(x), distance="soft_dtw")

@@ -323,3 +323,26 @@ def test_exact_fixture_reference_auctions_are_tie_free(golden):
     cert = O.auction_tie_certificate(s)
     assert np.array_equal(cert["torch"], cert["stable"])
     assert np.array_equal(cert["stable"], lab[:, 0])
+
+
+def test_pairwise_cosine_and_cosine_kmeans_match_reference(golden):
+    """pairwise_cosine (balancekmeans/__init__.py:625-655) and KMeans(distance='cosine') fits / predict
+    (:279-280, 511-512) restated by the oracle against the reference's outputs (tests/golden/cosine.npz)."""
+    g = golden("cosine")
+    x, c = _data.cosine_inputs(g)
+    np.testing.assert_allclose(O.pairwise_cosine(x, c), g["d"], rtol=0, atol=2e-6)
+
+    def rng(seed):
+        gen = torch.Generator().manual_seed(seed)
+        np.random.seed(seed)
+        return O.LegacyRNG(seed, lambda n: torch.randint(n, (1,), generator=gen).item())
+
+    c1, a1 = O.kmeans_fit(x, 8, rng(31), iter_limit=4, balanced=True, dist_fn=O.pairwise_cosine)
+    assert np.array_equal(a1, g["fit_bal_assign"])
+    np.testing.assert_allclose(c1, g["fit_bal_centers"], rtol=1e-5, atol=1e-5)
+    assert np.array_equal(O.pairwise_cosine(x, c1).argmin(1), g["pred"])
+    c2, a2 = O.kmeans_fit(x, 8, rng(32), iter_limit=3, balanced=False, dist_fn=O.pairwise_cosine)
+    assert np.array_equal(a2, g["fit_unbal_assign"])
+    np.testing.assert_allclose(c2, g["fit_unbal_centers"], rtol=1e-5, atol=1e-5)
+    c3, _ = O.kmeans_fit(x, 8, rng(33), iter_limit=4, balanced=True, min_loss_target=64, dist_fn=O.pairwise_cosine)
+    np.testing.assert_allclose(c3, g["fbml_centers"], rtol=1e-5, atol=1e-5)
