@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--jobs", type=int, default=100000)
     ap.add_argument("--workers", type=int, default=1280)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--sharded", action="store_true",
+                    help="the row-sharded protocol (ShardedAuction + rqsid_dauction_*) over a world-1 process group "
+                         "(RQSID_DAUCTION_LIST=0: every round sweeps)")
     ap.add_argument("--segments", type=int, default=0,
                     help="S > 0: S equal segments, each its own K-worker auction (ops.seg_auction, the lockstep "
                          "sub-fits' form)")
@@ -35,6 +38,18 @@ def main():
         def run():
             _, rr = ops.seg_auction(w, a.workers, lay)
             return int(rr.max().item())
+    elif a.sharded:
+        import os
+        import torch.distributed as dist
+        from generative_ranking_recommender_amd.distributed import GpuAuctionPasses, ShardedAuction
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        c = torch.randn(a.workers, 512, device="cuda", generator=g)
+        w = ops.auction_scores(x, c, half=True)
+
+        def run():
+            return ShardedAuction().run(GpuAuctionPasses(w, a.jobs), a.jobs, a.workers)[1]
     else:
         c = torch.randn(a.workers, 512, device="cuda", generator=g)
         w = ops.auction_scores(x, c, half=True)
@@ -47,7 +62,8 @@ def main():
         rounds = run()
         torch.cuda.synchronize()
         dt = time.time() - t
-        print(json.dumps({"jobs": a.jobs, "workers": a.workers, "segments": a.segments, "rounds": rounds, "s": round(dt, 3),
+        print(json.dumps({"jobs": a.jobs, "workers": a.workers, "segments": a.segments, "sharded": a.sharded,
+                          "rounds": rounds, "s": round(dt, 3),
                           "ms_per_round": round(1e3 * dt / max(rounds, 1), 4),
                           "W_GB": round(2 * a.jobs * a.workers / 1e9, 3)}), flush=True)
 
