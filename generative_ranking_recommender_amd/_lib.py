@@ -38,12 +38,13 @@ SIGNATURES = {
     "rqsid_version": (c_i32, []),
     "rqsid_last_error": (c_char_p, []),
     "rqsid_prepare_centers": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp]),
+    "rqsid_prepare_centers_hi": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
     "rqsid_bucket_workspace_bytes": (c_i64, [c_i64, c_i32]),
     "rqsid_bucket": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "rqsid_assign_tile_rows": (c_i32, []),
     "rqsid_assign_workspace_bytes": (c_i64, [c_i64]),
     "rqsid_assign": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_i64,
-                             c_vp, c_vp, c_vp, c_i32,
+                             c_vp, c_vp, c_vp, c_vp, c_i32,
                              c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
                              c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_vp, c_vp, c_i32, c_vp, c_i64, c_vp]),

@@ -1351,6 +1351,13 @@ __global__ __launch_bounds__(64) void mfma_probe_kernel(const uint16_t* __restri
   for (int v = 0; v < 16; ++v) d[((v & 3) + 8 * (v >> 2) + 4 * hh) * 32 + i] = acc[v];
 }
 
+// the hi terms of the interleaved table, contiguous per centre: each 32-dim chunk of c16 is 4 16-B pieces of hi
+// terms then 4 of lo terms, so hi piece i is c16 piece 8 (i / 4) + i % 4
+__global__ __launch_bounds__(256) void centers_hi_kernel(const uint4* __restrict__ c16, int64_t n, uint4* __restrict__ hi) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    hi[i] = c16[(i >> 2) * 8 + (i & 3)];
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -1443,6 +1450,16 @@ int rqsid_prepare_centers(const float* centers, int64_t k, int32_t dim, uint16_t
   return check_launch("prepare_centers");
 }
 
+int rqsid_prepare_centers_hi(const uint16_t* c16, int64_t k, int32_t dim, uint16_t* c16_hi, void* stream) {
+  if (!c16 || !c16_hi || k < 0 || dim <= 0 || dim % kChunk || dim > kMaxDim)
+    return fail(RQSID_E_ARG, "prepare_centers_hi: bad arguments (k=%lld dim=%d)", (long long)k, dim);
+  if (k == 0) return RQSID_OK;
+  const int64_t n = k * dim / 8;  // 16-B pieces of the hi table
+  hipLaunchKernelGGL(centers_hi_kernel, dim3((unsigned)grid_cap(cdiv(n, 256), 8192)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const uint4*>(c16), n, reinterpret_cast<uint4*>(c16_hi));
+  return check_launch("prepare_centers_hi");
+}
+
 int32_t rqsid_assign_tile_rows(void) { return kTileRows; }
 
 // workspace: [0,256) counters and store sinks | WorkItem[n_rows] | tile->segment map i32[n_rows]
@@ -1455,7 +1472,8 @@ int64_t rqsid_assign_workspace_bytes(int64_t n_rows) {
 
 int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row_index, int32_t n_segments,
                  const int32_t* seg_row_off, const int32_t* seg_tile_off, int64_t max_tiles, const float* centers,
-                 const uint16_t* c16, const float* c_meta, int32_t n_centers, const int32_t* cand_base,
+                 const uint16_t* c16, const uint16_t* c16_hi, const float* c_meta, int32_t n_centers,
+                 const int32_t* cand_base,
                  const int32_t* cand_count, int32_t cand_count_max, const int32_t* cand_idx,
                  const int32_t* cand_lid, const uint8_t* seg_flags, int32_t res_levels, int32_t res_normalize, const float* ca,
                  const int32_t* seg_ca, const float* cb, const int32_t* seg_cb, const float* den_in,
@@ -1485,6 +1503,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   p.seg_tile_off = seg_tile_off;
   p.centers = centers;
   p.c16 = c16;
+  p.c16h = c16_hi;
   p.c_meta = c_meta;
   p.n_centers = n_centers;
   p.cand_base = cand_base;

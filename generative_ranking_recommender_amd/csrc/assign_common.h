@@ -45,6 +45,8 @@ struct AssignParams {
   const int32_t* seg_tile_off;
   const float* centers;
   const uint16_t* c16;   // fp16 bits [k][dim/32][2][32]: per chunk hi then lo terms (rqsid_prepare_centers)
+  const uint16_t* c16h;  // NULL, or the hi terms alone [k][dim] (rqsid_prepare_centers_hi): the 1-term streamed
+                         // screens gather their 64-B pieces from it, half the cache lines of the interleaved table
   const float* c_meta;   // [k+1] float4: per centre |c|^2, |c|, |c - (hi + lo 2^-12) 2^-s|, |c - hi 2^-s|; row k: 2^-s
   int32_t n_centers;
   const int32_t* cand_base;

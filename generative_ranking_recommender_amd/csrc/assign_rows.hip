@@ -148,7 +148,8 @@ __global__ __launch_bounds__(W * 64, 2) void assign_rows_kernel(AssignParams p, 
         const int il = (wave * P + j) * 16 + (lane >> 2);
         const int g = gidx[blk * kCB + il];
         const int sl = (lane & 3) ^ ((il >> 2) & 3);
-        const _Float16* src = reinterpret_cast<const _Float16*>(p.c16) + (int64_t)g * 2 * kRDim + c * 64 + sl * 8;
+        const _Float16* src = p.c16h ? reinterpret_cast<const _Float16*>(p.c16h) + (int64_t)g * kRDim + c * 32 + sl * 8
+                                     : reinterpret_cast<const _Float16*>(p.c16) + (int64_t)g * 2 * kRDim + c * 64 + sl * 8;
         dma16(src, __builtin_amdgcn_readfirstlane(lds0 + (uint32_t)((q % S) * L::kCStage + (wave * P + j) * 1024)));
       }
     };

@@ -650,6 +650,7 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
   const float tgw = __uint_as_float(uni(__float_as_uint(trow[2])));
   const float tgy = __uint_as_float(uni(__float_as_uint(trow[3])));
   int* const dummy = p.work_count + 16;                 // sink of the fixed-count stores
+  const uint32_t cunits = (!T3 && p.c16h) ? 64u : 128u;  // 16-B units per centre row of the table gathered
 
   // ---- header pipeline pieces -------------------------------------------------------------
   // level 1: row indices (wave w: rows 32w..32w+31, lanes 0..31), candidate indices (wave w:
@@ -707,7 +708,7 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
     for (int j = 0; j < kCI; ++j) {
       const int k = (gw * kCI + j) * 16 + (lane >> 2);
       const int sl = (lane & 3) ^ ((k >> 2) & 3);
-      n.ci[j] = (uint32_t)cand_of(H, par, k) * 128u + (uint32_t)sl;
+      n.ci[j] = (uint32_t)cand_of(H, par, k) * cunits + (uint32_t)sl;
     }
   };
   // level 2: |c|^2 and |c| of the candidates (SoA, gathered from meta), den_in of the rows (RL2 NORM)
@@ -726,12 +727,16 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
 
   // ---- ring: this wave's share of chunk j (tile-relative; 16, 17 = the next tile's 0, 1) ----------
   const char* const xbase = reinterpret_cast<const char*>(p.x);
-  const char* const cbase16 = reinterpret_cast<const char*>(p.c16);
+  // the 1-term screen gathers hi pieces: from the hi-only table when present (a 1-KiB row per centre, 64 B per
+  // chunk), else from the interleaved table (2 KiB per centre, 128 B per chunk: hi then lo)
+  const bool hi_tab = !T3 && p.c16h;
+  const char* const cbase16 = reinterpret_cast<const char*>(hi_tab ? p.c16h : p.c16);
+  const int cchunk = hi_tab ? kSC * 2 : kSC * 4;  // bytes per chunk of a centre row
   auto addr = [](const char* base, uint32_t unit) -> const void* { return base + (uint64_t)unit * 16u; };
   int qb = 0;  // row stage of this tile's chunk 0 (16 % 3 != 0: walks on across tiles)
   auto issue_c = [&](const Next& n, int j) __attribute__((always_inline)) {  // group 1: chunk j's centres
     const uint32_t sc = lds0 + L::kC + (j & 1) * L::kCStage;
-    const char* cb = cbase16 + (j & 15) * (kSC * 4);  // c16 row: per chunk 64 B hi then 64 B lo
+    const char* cb = cbase16 + (j & 15) * cchunk;  // chunk j's piece of every centre row
 #pragma unroll
     for (int q = 0; q < kCI; ++q) dma16(addr(cb, n.ci[q]), uni(sc + (gw * kCI + q) * 1024));
     if (T3) {

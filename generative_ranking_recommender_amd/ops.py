@@ -47,6 +47,9 @@ def centroid_tile_rows() -> int:
 
 
 kMaxList = 8  # candidates a screen can list per row (assign_common.h)
+# the 1-term streamed screens gather centre pieces from a hi-only copy of the table (RQSID_HI_TABLE=0: from the
+# interleaved table, for A/B); read once at import
+HI_TABLE = __import__("os").environ.get("RQSID_HI_TABLE", "1") != "0"
 
 
 @dataclass
@@ -56,6 +59,7 @@ class PreparedCenters:
     c16: torch.Tensor          # int16 [K, D/32, 2, 32]: per 32-dim chunk the hi then lo fp16 terms of c 2^s
     meta: torch.Tensor         # f32 [K+1, 4]: |c|^2, |c|, |2-term residual|, |1-term residual|; row K: 2^-s
     nearest_cand: Optional["Candidates"] = None  # nearest()'s candidate list (duplicates dropped), built once
+    c16h: Optional[torch.Tensor] = None  # int16 [K, D]: the hi terms alone (the 1-term streamed screens' source)
 
     @property
     def k(self) -> int:
@@ -74,7 +78,11 @@ def prepare_centers(c: torch.Tensor) -> PreparedCenters:
     meta = torch.empty((k + 1, 4), dtype=torch.float32, device=c.device)
     _lib.check(lib().rqsid_prepare_centers(_ptr(c), k, d, _ptr(c16), _ptr(meta), _stream()),
                "rqsid_prepare_centers")
-    return PreparedCenters(c, c16, meta)
+    c16h = None
+    if HI_TABLE and k > 0:
+        c16h = torch.empty((k, d), dtype=torch.int16, device=c.device)
+        _lib.check(lib().rqsid_prepare_centers_hi(_ptr(c16), k, d, _ptr(c16h), _stream()), "rqsid_prepare_centers_hi")
+    return PreparedCenters(c, c16, meta, c16h=c16h)
 
 
 @dataclass
@@ -241,7 +249,7 @@ def assign(x: torch.Tensor, pc: PreparedCenters, buckets: Buckets, cand: Candida
     _lib.check(lib().rqsid_assign(
         _ptr(x), n, d, _ptr(buckets.row_index), buckets.n_segments, _ptr(buckets.seg_row_off),
         _ptr(buckets.seg_tile_off), buckets.max_tiles,
-        _ptr(pc.centers), _ptr(pc.c16), _ptr(pc.meta), pc.k,
+        _ptr(pc.centers), _ptr(pc.c16), _ptr(pc.c16h), _ptr(pc.meta), pc.k,
         _ptr(cand.base), _ptr(cand.count), cand.count_max, _ptr(cand.idx), _ptr(cand.lid), _ptr(cand.flags),
         0 if f is None else f.levels, 0 if f is None else int(f.normalize),
         None if f is None else _ptr(f.ca), None if f is None else _ptr(f.seg_ca),

@@ -50,6 +50,11 @@ const char* rqsid_last_error(void);
  * balancekmeans/__init__.py:576-603. */
 int rqsid_prepare_centers(const float* centers, int64_t k, int32_t dim,
                           uint16_t* c16, float* c_meta, void* stream);
+/* The hi terms of a prepared table alone, c16_hi [k][dim] fp16 (1 KiB per 512-d centre): the 1-term streamed
+ * screens (the ping-pong and row-resident forms) gather their 64-B centre pieces from it when rqsid_assign
+ * gets it, touching half the cache lines of the interleaved table (the XL last level's 5120 candidates: 5 MB
+ * instead of 10 MB against a 4-MB XCD L2). */
+int rqsid_prepare_centers_hi(const uint16_t* c16, int64_t k, int32_t dim, uint16_t* c16_hi, void* stream);
 
 /* Counting sort of rows by segment key (keys in [0, n_segments)).
  * Outputs seg_row_off[S+1], seg_tile_off[S+1] (exclusive scan of
@@ -103,6 +108,7 @@ int32_t rqsid_assign_tile_rows(void);
  * Errors: RQSID_E_ARG / RQSID_E_WORKSPACE before any launch; RQSID_E_LAUNCH for a HIP launch failure
  * or, on the opt-in centre-resident screen (RQSID_SCREEN_VARIANT=6), when a wave's capped role wait
  * gave up (device error word read back after the call; the IDs it left are not returned as valid).
+ * c16_hi: NULL or rqsid_prepare_centers_hi's table of the same centres (only where-from changes, never the IDs).
  * Workspace bytes [240, 244) are a sticky error word the caller zeroes when it allocates the workspace
  * (every call zeroes only [0, 240)): each list write whose index comes from a device counter (the
  * re-score compaction, the overflow list) is bounded by its slot's capacity, and a write that would fall
@@ -111,7 +117,7 @@ int64_t rqsid_assign_workspace_bytes(int64_t n_rows);
 int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row_index,
                  int32_t n_segments, const int32_t* seg_row_off, const int32_t* seg_tile_off,
                  int64_t max_tiles,
-                 const float* centers, const uint16_t* c16, const float* c_meta,
+                 const float* centers, const uint16_t* c16, const uint16_t* c16_hi, const float* c_meta,
                  int32_t n_centers,
                  const int32_t* cand_base, const int32_t* cand_count, int32_t cand_count_max,
                  const int32_t* cand_idx, const int32_t* cand_lid, const uint8_t* seg_flags,

@@ -602,3 +602,26 @@ def test_nearest_with_many_duplicate_centres():
     assert (got[:500] == dup.min()).all()
     sel = np.arange(0, n, 7)
     assert (got[sel] == exact_ids(x[sel], c)).all()
+
+
+@pytest.mark.parametrize("form", ["default", "pp88", "rows443"])
+@pytest.mark.parametrize("shape", ["prod", "xl"])
+def test_hi_only_centre_table_equals_interleaved(shape, form):
+    """The 1-term streamed screens gather their centre pieces from the hi-only table (rqsid_prepare_centers_hi)
+    by default; the interleaved table gives the same IDs on every level (ping-pong and row-resident forms, the
+    PROD and XL codebook shapes), and the hi table is the interleaved table's hi halves."""
+    need = (128, 128, 256) if shape == "prod" else (256, 256, 512)
+    cb = synth.encode_codebooks(seed=99, need=need, n_cand=2560 if shape == "prod" else 5120)
+    x = gpu(synth.mixture_rows(0, 60000))
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], list(need),
+                    match=torch.from_numpy(cb["match"]), semantics=HIERARCHICAL_TRAIN, device=DEV)
+    env = {"default": {}, "pp88": STREAMED.get("pp88", {}), "rows443": {"RQSID_SCREEN_VARIANT": "8",
+                                                                          "RQSID_ROWS_SHAPE": "443"}}[form]
+    assert all(pc.c16h is not None for pc in enc.pcs)
+    c16 = enc.pcs[2].c16.view(enc.pcs[2].k, -1, 2, 32)
+    assert torch.equal(enc.pcs[2].c16h.view(enc.pcs[2].k, -1, 32), c16[:, :, 0, :])
+    a = _with_env(env, lambda: enc.encode(x).cpu().numpy())
+    for pc in enc.pcs:
+        pc.c16h = None
+    b = _with_env(env, lambda: enc.encode(x).cpu().numpy())
+    assert (a == b).all(), f"{int((a != b).any(1).sum())} rows differ between the hi-only and interleaved tables"
