@@ -1956,6 +1956,10 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   // into a counter zeroed after each read.  The round number lives on the device, so one captured block
   // (a HIP graph of kPoll rounds) replays for every block: the auction is launch-bound at small N.
   constexpr int kPoll = 8;
+  // list-only blocks are longer: their rounds are a few launches each, and the host's readback and launch
+  // between two blocks (tens of us) cost as much as several rounds; a failed list replays the block's first
+  // kPoll rounds in full from its snapshot, then the loop goes on from there
+  constexpr int kPollList = 32;
   // lean rounds leave out the two-pass kernels of missed workers (five launches of a few us each, empty
   // in most rounds); a lean block runs from a snapshot of the round state and is replayed with the full
   // rounds when any worker missed in it, so the result is the full rounds' in every case
@@ -2024,9 +2028,10 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     hipGraphExec_t ex = nullptr;
     hipStream_t cs = nullptr;
     hipGraph_t graph = nullptr;
+    const int nr = list_only ? kPollList : kPoll;
     if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) == hipSuccess) {
       if (hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed) == hipSuccess) {
-        for (int i = 0; i < kPoll; ++i) launch_round(cs, i == kPoll - 1, lean, list_only);
+        for (int i = 0; i < nr; ++i) launch_round(cs, i == nr - 1, lean, list_only);
         if (hipStreamEndCapture(cs, &graph) == hipSuccess && graph) {
           if (hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0) != hipSuccess) ex = nullptr;
           (void)hipGraphDestroy(graph);
@@ -2046,8 +2051,9 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   if (fill_async(a.live_count, 0, 4, st) != hipSuccess) rc = fail(RQSID_E_LAUNCH, "seg_auction: memset");
   bool try_lean = false;  // round 0 misses everywhere (thresholds start at key 0)
   for (int done = 0; rc == RQSID_OK && (max_rounds <= 0 || done < max_rounds);) {
-    const int n = max_rounds > 0 ? std::min(kPoll, max_rounds - done) : kPoll;
-    const bool lonly = try_list && exec_list && n == kPoll;
+    int n = max_rounds > 0 ? std::min(kPoll, max_rounds - done) : kPoll;
+    const bool lonly = try_list && exec_list && (max_rounds <= 0 || max_rounds - done >= kPollList);
+    if (lonly) n = kPollList;
     const bool lean = !lonly && try_lean && exec_lean && n == kPoll;
     (lonly ? n_list : lean ? n_lean : n_full) += 1;
     if (fill_async(a.live_count + 2, 0, 8, st) != hipSuccess) {
@@ -2091,6 +2097,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
       try_lean = false;
       try_list = false;
       ++n_replay;
+      n = kPoll;  // the replayed block's rounds (a list-only block's later rounds are not run)
     } else {
       try_lean = n_multi > 0;
       try_list = host[3] == 0;  // every list held through this block
