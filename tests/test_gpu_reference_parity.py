@@ -503,10 +503,14 @@ def test_cosine_distance_kmeans_against_reference(golden):
     km3 = bk.KMeans(n_clusters=8, device=DEV, balanced=True)
     km3.fit_by_min_loss(torch.from_numpy(x), target_nodes_num=64, distance="cosine", iter_limit=4, tqdm_flag=False)
     c3 = km3.cluster_centers.cpu().numpy()
+    # fit_by_min_loss keeps the centres of its smallest overflow loss (:330-340); after a tie-born step the
+    # two runs keep different iterations' centres, so only the objective it minimises is compared
     n3, n3r = O.pairwise_cosine(x, c3).argmin(1), O.pairwise_cosine(x, g["fbml_centers"]).argmin(1)
-    assert total(c3, n3) <= total(g["fbml_centers"], n3r) * (1 + 5e-3) + 1e-3
+    loss = lambda n: int(np.maximum(np.bincount(n, minlength=8) - 64, 0).sum())  # noqa: E731
+    assert loss(n3) <= loss(n3r) + 8
     report("cosine_kmeans", fit_identical=bool(np.array_equal(a, g["fit_bal_assign"])),
            agree=float((a == g["fit_bal_assign"]).mean()), total_ref=t_ref, total_gpu=t_gpu,
-           score_flips=int(diff.sum()))
+           unbal_agree=float((a2 == g["fit_unbal_assign"]).mean()), fbml_loss_ref=loss(n3r), fbml_loss_gpu=loss(n3),
+           fbml_max_center_diff=float(np.abs(c3 - g["fbml_centers"]).max()), score_flips=int(diff.sum()))
     with pytest.raises(NotImplementedError):
         bk.KMeans(n_clusters=8, device=DEV).fit(torch.from_numpy(x), distance="soft_dtw")
