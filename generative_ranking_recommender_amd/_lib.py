@@ -78,6 +78,7 @@ SIGNATURES = {
     "rqsid_dauction_bid": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "rqsid_dauction_resolve": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "rqsid_dauction_end_round": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    "rqsid_dauction_debug": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "rqsid_dauction_list_pass": (c_i32, [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_i64, c_vp]),
     "rqsid_greedy_match": (c_i32, [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "rqsid_mfma_probe": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),

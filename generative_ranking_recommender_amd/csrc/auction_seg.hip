@@ -2635,6 +2635,36 @@ int rqsid_dauction_end_round(const uint16_t* scores, int32_t n_workers, int64_t 
   return check_launch("dauction_end_round");
 }
 
+// diagnostics (tools/auction_bench.py --sharded with RQSID_DAUCTION_STATS=1): out u32[8] = {slot mode, round,
+// max list entries, mean list entries, worker 0's lkb, worker 0's T, overflow word, lists over capacity}
+__global__ void da_debug_kernel(SegAuction a, uint32_t* out) {
+  uint64_t sum = 0;
+  uint32_t mx = 0, over = 0;
+  for (int w = 0; w < a.K; ++w) {
+    const uint32_t n = a.lcnt[(int64_t)w * kAbovePad];
+    sum += n;
+    mx = n > mx ? n : mx;
+    over += n > (uint32_t)a.dcap ? 1u : 0u;
+  }
+  out[0] = a.dmode[0];
+  out[1] = (uint32_t)*a.round_dev;
+  out[2] = mx;
+  out[3] = (uint32_t)(sum / (uint64_t)a.K);
+  out[4] = a.lkb[0];
+  out[5] = a.sel[2];
+  out[6] = a.hist[(int64_t)a.K * 256];
+  out[7] = over;
+}
+
+int rqsid_dauction_debug(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global, uint32_t* out,
+                         void* workspace, int64_t workspace_bytes, void* stream) {
+  SegAuction a;
+  int rc = dstate(a, scores, n_workers, n_local, n_global, workspace, workspace_bytes);
+  if (rc) return rc;
+  hipLaunchKernelGGL(da_debug_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, a, out);
+  return check_launch("dauction_debug");
+}
+
 // the list kernels of one pass alone, for list-only slots (the sweep kernels of hist / eqcount / bid are not
 // launched: at K = 2560 over 6.25M jobs each such launch costs ~0.2 ms of dispatch even when every block exits):
 // step -1 starts the slot (a sweep slot turns void), 0 / 1 the histograms, 2 the equal-value counts, 3 the

@@ -328,6 +328,12 @@ class GpuAuctionPasses:
         """Still bidding (host sync): end_round clears it once the reduced `have` covers every job."""
         return bool(int(self._flag.item()) & 1)
 
+    def debug(self) -> list:
+        """{mode, round, longest list, mean list, lkb[0], T[0], overflow word, lists over capacity} (host sync)"""
+        out = torch.zeros(8, dtype=torch.int32, device=self.w.device)
+        ops._lib.check(self.lib.rqsid_dauction_debug(*self._args(), ops._ptr(out), *self._tail()), "rqsid_dauction_debug")
+        return out.cpu().tolist()
+
     def lists_hold(self) -> bool:
         """The coming slot runs from the bid lists (host sync; the same on every rank: it is decided from
         reduced data only)."""
@@ -338,6 +344,9 @@ class GpuAuctionPasses:
 
     def result(self) -> torch.Tensor:
         return self.out[:self.n_local]
+
+
+_STATS = __import__("os").environ.get("RQSID_DAUCTION_STATS", "0") not in ("", "0")
 
 
 class ShardedAuction:
@@ -412,6 +421,8 @@ class ShardedAuction:
                 return passes.result(), passes.rounds_run()
             if max_rounds and issued >= max_rounds:
                 raise RuntimeError(f"auction: no complete assignment after {max_rounds} rounds")
+            if _STATS and hasattr(passes, "debug"):
+                print("dauction slot", issued, passes.debug(), flush=True)
             if lists is not None:
                 # the next slots launch the list kernels alone while the lists hold (a slot that meets a sweep
                 # round is void and the poll after it returns to full slots); every rank reads the same mode

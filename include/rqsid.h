@@ -266,6 +266,11 @@ int64_t rqsid_dauction_workspace_bytes(int64_t n_local, int32_t n_workers);
  * list_pass(0), sum, select(0), list_pass(1), sum, select(1), list_pass(2), gather, list_pass(3, rank_off),
  * resolve, sum, end_round: the same collectives without launching the sweep kernels; a list-only slot that
  * meets a sweep round is void (nothing changes) and the caller returns to full slots at its next poll. */
+/* Diagnostics of the row-sharded list state: out (device u32[8]) = {coming slot's mode, round, longest list,
+ * mean list length, worker 0's list base key, worker 0's threshold key, summed overflow word, lists over
+ * capacity}. */
+int rqsid_dauction_debug(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global, uint32_t* out,
+                         void* workspace, int64_t workspace_bytes, void* stream);
 int rqsid_dauction_list_pass(const uint16_t* scores, int32_t n_workers, int64_t n_local, int64_t n_global,
                              int32_t step, const uint32_t* rank_off, void* workspace, int64_t workspace_bytes,
                              void* stream);
