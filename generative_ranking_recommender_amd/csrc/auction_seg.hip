@@ -2454,9 +2454,9 @@ int dstate(SegAuction& a, const uint16_t* scores, int32_t k, int64_t n_local, in
   a.chunk_off = (const int32_t*)(p + 64);
   a.rounds = (int32_t*)(p + 128);
   a.dmode = (uint32_t*)(p + 192);  // [0] slot mode (the caller may poll it), [1] sweep-slot flag
-  a.any_miss = a.dmode + 1;        // (the sweep kernels exit unless it is set)
   Carve c{p + kDHeader};
   carve(a, c, n_local, k, 1, nch, false, true);
+  a.any_miss = a.dmode + 1;        // after carve (which clears it): the sweep kernels exit unless it is set
   if (wsb < kDHeader + c.used) return fail(RQSID_E_WORKSPACE, "dauction: workspace too small");
   return RQSID_OK;
 }
