@@ -304,6 +304,8 @@ def config0(dev, rows=100_000, cpu_rounds=40):
                       "against": "oracle/rq_oracle.py nearest(exact=True) of the trained centres, evenly spaced rows",
                       "cluster_sizes_min_max": [int(np.bincount(ids, minlength=128).min()),
                                                 int(np.bincount(ids, minlength=128).max())]}}
+    if cpu_rounds <= 0:  # (tools/config0_time.py: the GPU fit alone)
+        return out
     # the CPU restatement of one iteration (the reference's own arithmetic, numpy)
     rng = np.random.default_rng(0)
     c = xs[rng.choice(rows, 128, replace=False)]

@@ -32,6 +32,7 @@ constexpr int kKG = 16;        // workers per block
 constexpr int kCh = 1024;      // jobs per chunk
 constexpr int kJPT = kCh / 256;
 constexpr int kAbovePad = 32;  // u32 per worker in SegAuction::above
+constexpr int kRd = 16;        // first-level arrival counters of the fused round end (SegAuction::rdone)
 static_assert(kJPT == 4 && kJPT * kKG == 64, "load_chunk<true> takes 4 jobs per lane; sa_bid_kernel keeps one deferral bit per (job slice, worker) in two u32, "
               "and its 64 x 4 eqm slots are zeroed by the 256 threads");
 
@@ -1075,17 +1076,26 @@ __device__ __forceinline__ void resolve_chunk(const SegAuction& a, const ChunkIn
     const uint32_t tot = wc[0] + wc[1] + wc[2] + wc[3];
     if (a.rdone) {
       // one 64-bit atomic carries both the arrival and the count, so the last block to arrive sees every
-      // other block's count in the value it gets back (no fence between two atomics needed)
-      const unsigned long long old = atomicAdd(a.rdone, (1ull << 32) | tot);
-      if ((old >> 32) == (unsigned long long)(gridDim.x - 1)) {
-        const uint32_t have = (uint32_t)old + tot;
+      // other block's count in the value it gets back (no fence between two atomics needed).  Two levels:
+      // block b arrives at counter 1 + b % kRd, the last of those at counter 0 (same-address atomics
+      // serialise at ~12 ns each: 977 blocks of a 1M-job auction on one word cost 12 us per round)
+      const uint32_t G = gridDim.x, sub = blockIdx.x % kRd;
+      const uint32_t nsub = (G - sub + kRd - 1) / kRd, ntop = min(G, (uint32_t)kRd);
+      unsigned long long* const c1 = a.rdone + 16 * (1 + sub);  // (one 128-B line per counter)
+      const unsigned long long o1 = atomicAdd(c1, (1ull << 32) | tot);
+      if ((o1 >> 32) != (unsigned long long)(nsub - 1)) return;
+      atomicExch(c1, 0ull);
+      const uint32_t part = (uint32_t)o1 + tot;
+      const unsigned long long old = atomicAdd(a.rdone, (1ull << 32) | part);
+      if ((old >> 32) == (unsigned long long)(ntop - 1)) {
+        const uint32_t have = (uint32_t)old + part;
         *a.round_dev += 1;
         if (a.any_miss) *a.any_miss = 0;
         if (a.lany) *a.lany = 0;
         a.rounds[0] += 1;
         const bool live = (int64_t)have != (int64_t)(a.seg_off[1] - a.seg_off[0]);
         if (!live) a.flag[0] &= ~kLive;
-        *a.rdone = 0;
+        atomicExch(a.rdone, 0ull);
         if (a.rcount && live) atomicAdd(a.live_count, 1u);
       }
     } else if (tot) {
@@ -1834,7 +1844,7 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.lstart = ls ? std::max(1, atoi(ls)) : K >= kListWideK ? kListStartWide : kListStart;
   const char* ed = getenv("RQSID_LIST_DELTA");
   a.ldelta = ed ? std::min(128, std::max(1, atoi(ed))) : kListDelta;
-  a.rdone = guess && S == 1 && a.n_multi == 1 ? c.take<unsigned long long>(1) : nullptr;
+  a.rdone = guess && S == 1 && a.n_multi == 1 ? c.take<unsigned long long>(16 * (1 + kRd)) : nullptr;
   const char* es = getenv("RQSID_LIST_STATS");
   a.lstat = list && es && atoi(es) ? c.take<uint32_t>(8) : nullptr;
   if (dlist) {  // the row-sharded auction's lists: one rank's share, 8 * (N / K) + 256 entries per worker
@@ -1917,7 +1927,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
     return fail(RQSID_E_LAUNCH, "seg_auction: pinned readback buffer");
   }
   int rc = RQSID_OK;
-  if (fill_async(a.live_count, 0, 16, st) != hipSuccess || (a.rdone && fill_async(a.rdone, 0, 8, st) != hipSuccess))
+  if (fill_async(a.live_count, 0, 16, st) != hipSuccess || (a.rdone && fill_async(a.rdone, 0, 128 * (1 + kRd), st) != hipSuccess))
     return fail(RQSID_E_LAUNCH, "seg_auction: memset");
   hipLaunchKernelGGL(sa_seg_init_kernel, dim3(gs), dim3(256), 0, st, a, active);
   hipLaunchKernelGGL(sa_multi_index_kernel, dim3(1), dim3(1024), 0, st, a);
