@@ -748,8 +748,10 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
   auto issue_x = [&](const Next& n, int j) __attribute__((always_inline)) {  // this group's rows of chunk j
     const uint32_t sx = lds0 + L::kX + (grp * 3 + (qb + j) % 3) * L::kXG + gw * 4096;
     const char* xb = xbase + (j & 15) * (kSC * 4);
+#ifndef RQSID_AB_NOROWDMA  // (timing probe only: no row traffic, wrong results)
 #pragma unroll
     for (int i = 0; i < 4; ++i) dma16_nt(addr(xb, n.xi[i]), uni(sx + i * 1024));
+#endif
   };
 
   // ---- first tile: synchronous header ----------------------------------------------------------
@@ -877,19 +879,24 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
         U = fminf(U, __shfl_xor(U, 32));
         const float Up = fmaf(fabsf(U), 0x1p-22f, U) + 1.2e-38f;
         const f2 upv = {Up, Up};
+        // pass bits: NT independent 16-bit chains (one per candidate tile) the scheduler may interleave, then
+        // paired into words (tile 2w in the high half).  One chain through all NT tiles, sched-barriered per tile,
+        // was latency-bound on its dependent alignbits: 1.75 ms of the 7.5-ms PROD level 2 (tools/ab_build.sh
+        // RQSID_AB_EPI probes)
+        uint32_t pbt[NT];
+  #pragma unroll
+        for (int t = 0; t < NT; ++t) pbt[t] = 0u;
+  #pragma unroll
+        for (int v = 0; v < 16; v += 2)  // (v outer: the NT chains advance together)
+  #pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const f2 d = f2{acc[t][v], acc[t][v + 1]} - upv;
+            pbt[t] = __builtin_amdgcn_alignbit(pbt[t], __float_as_uint(d.x), 31);
+            pbt[t] = __builtin_amdgcn_alignbit(pbt[t], __float_as_uint(d.y), 31);
+          }
         uint32_t pbits[NT / 2];
   #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          __builtin_amdgcn_sched_barrier(0);
-          uint32_t b = (t & 1) ? pbits[t >> 1] : 0u;
-  #pragma unroll
-          for (int v = 0; v < 16; v += 2) {
-            const f2 d = f2{acc[t][v], acc[t][v + 1]} - upv;
-            b = __builtin_amdgcn_alignbit(b, __float_as_uint(d.x), 31);
-            b = __builtin_amdgcn_alignbit(b, __float_as_uint(d.y), 31);
-          }
-          pbits[t >> 1] = b;
-        }
+        for (int wd = 0; wd < NT / 2; ++wd) pbits[wd] = (pbt[2 * wd] << 16) | pbt[2 * wd + 1];
         // candidates beyond cnt (duplicates of the last one) never pass
         // (a lane half's candidates ascend with v, so a tile's valid values are a prefix of its 16 bits)
         if (H_.cnt < NT * 32) {
@@ -909,7 +916,15 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
           }
         }
         int k = -1;
+#if defined(RQSID_AB_EPI)  // (timing probes only, wrong results: 1 = no pass bits, 2 = no list decision)
+        uint32_t px = 0;
+        for (int q = 0; q < NT / 2; ++q) px ^= pbits[q];
+        if (RQSID_AB_EPI == 1) px = __float_as_uint(Up) | 1u;
+        k = __builtin_ctz(px | 0x80000000u);
+        if (true) {
+#else
         if (pass_decide(pbits, h, k, w)) {
+#endif
           out_l = k;
           out_g = cand_of(Hc, par_, k);
         } else {

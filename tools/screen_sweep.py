@@ -49,8 +49,10 @@ def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000)), reps=int(os.environ.ge
     e.record()
     torch.cuda.synchronize()
     ms = timer.mean_ms()
+    encmod.ops.assign = orig
+    enc.encode(x, count_rescored=True)
     print(f"lib={os.environ.get('RQSID_LIB', 'default')} variant={os.environ.get('RQSID_SCREEN_VARIANT', '0')} step={s.elapsed_time(e) / reps:.2f} ms " +
-          " ".join(f"{k}={v:.3f}" for k, v in sorted(ms.items())), flush=True)
+          " ".join(f"{k}={v:.3f}" for k, v in sorted(ms.items())) + f" rescored={list(enc.last_rescored)}", flush=True)
 
 
 if __name__ == "__main__":
