@@ -132,6 +132,7 @@ struct SegAuction {
   // one-segment auctions (single process): {blocks arrived << 32 | jobs with a bidder} of the round's resolve;
   // the last block to arrive ends the round (sa_round_end_kernel's work, one launch fewer per round)
   unsigned long long* rdone;
+  uint32_t* js;                  // (list rounds) per job {winner & 0xFFFF, cost bits}: one gather per listed job
   int32_t rcount;                // end-of-round: add the live count for the host's poll (a block's last round)
 };
 constexpr int64_t kListMaxJpw = 16384;  // one-block list rounds only while the average jobs per worker per segment is at most this
@@ -191,6 +192,17 @@ __device__ __forceinline__ uint16_t value_bits(int w, uint16_t wv, int32_t hbj, 
 __device__ __forceinline__ _Float16 value_h(int w, uint16_t wv, int32_t hbj, uint16_t cj) {
   const _Float16 r = __builtin_bit_cast(_Float16, wv);
   return hbj == w ? r : (_Float16)(r - __builtin_bit_cast(_Float16, cj));
+}
+
+// a job's last winner and cost from the packed word when the list rounds keep one (else the two arrays); the
+// packed word's winner is 16 bits (js is allocated only for K <= 65535), 0xFFFF = none
+__device__ __forceinline__ int32_t js_hb(const SegAuction& a, int64_t j) {
+  if (!a.js) return a.hb[j];
+  const uint32_t h = a.js[j] >> 16;
+  return h == 0xFFFFu ? -1 : (int32_t)h;
+}
+__device__ __forceinline__ uint16_t js_cost(const SegAuction& a, int64_t j) {
+  return a.js ? (uint16_t)(a.js[j] & 0xFFFFu) : a.cost[j];
 }
 
 __device__ __forceinline__ const uint16_t* wrow(const SegAuction& a, const ChunkInfo& ci, int w) {
@@ -274,6 +286,7 @@ __global__ __launch_bounds__(256) void sa_job_init_kernel(SegAuction a, int64_t 
     a.hb[j] = -1;
     a.nobid[j] = 0;
     a.key[j] = 0;
+    if (a.js) a.js[j] = 0xFFFF0000u;
   }
 }
 
@@ -1059,12 +1072,15 @@ __device__ __forceinline__ void resolve_chunk(const SegAuction& a, const ChunkIn
       out[j] = w;
       a.hb[j] = w;
       a.nobid[j] = 0;
-      a.cost[j] = f2h(h2f(c[t]) + h2f(bid));
+      const uint16_t cn = f2h(h2f(c[t]) + h2f(bid));
+      a.cost[j] = cn;
+      if (a.js) a.js[j] = ((uint32_t)w << 16) | cn;
       ++cnt;
     } else {
       out[j] = -1;
       a.hb[j] = -1;
       a.nobid[j] = 1;
+      if (a.js) a.js[j] = 0xFFFF0000u | c[t];
     }
   }
   // one same-address atomic per block, not per wave: a segment's chunks all count into have[s]
@@ -1341,7 +1357,7 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
   // the later passes read the list only
   for (uint32_t i = tid; i < n; i += kLT) {
     const uint2 e = L[i];
-    const uint32_t k = okey(value_bits(w, (uint16_t)e.y, a.hb[e.x], a.cost[e.x]));
+    const uint32_t k = okey(value_bits(w, (uint16_t)e.y, js_hb(a, e.x), js_cost(a, e.x)));
     L[i].y = (e.y & 0xFFFFu) | (k << 16);
     if (k >= kb) atomicAdd(&hst[k >> 8], 1u);
   }
@@ -1440,7 +1456,7 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
     } else if (k == T && need && j <= J) {
       bid = eps;
     }
-    if (ret && a.hb[j] == w) bid = eps;  // retention: the previous winner bids eps on its job
+    if (ret && js_hb(a, j) == w) bid = eps;  // retention: the previous winner bids eps on its job
     if (bid) atomicMax(&a.key[j], (bid << 16) | (0xFFFFu - (uint32_t)w));
   }
   if (tid == 0) {
@@ -1515,7 +1531,7 @@ __global__ __launch_bounds__(256) void sa_mlist_pass_kernel(SegAuction a) {
     for (uint32_t i = i0 + tid; i < i1; i += 256) {
       if (STEP == 0) {
         const uint2 e = L[i];
-        const uint32_t k = okey(value_bits(w, (uint16_t)e.y, a.hb[e.x], a.cost[e.x]));
+        const uint32_t k = okey(value_bits(w, (uint16_t)e.y, js_hb(a, e.x), js_cost(a, e.x)));
         L[i].y = (e.y & 0xFFFFu) | (k << 16);
         if (k >= kb) atomicAdd(&hst[k >> 8], 1u);
       } else {
@@ -1562,7 +1578,7 @@ __global__ __launch_bounds__(256) void sa_mlist_pass_kernel(SegAuction a) {
       }
       if (lo < need) bid = eps;
     }
-    if (ret && a.hb[j] == w) bid = eps;  // retention: the previous winner bids eps on its job
+    if (ret && js_hb(a, j) == w) bid = eps;  // retention: the previous winner bids eps on its job
     if (bid) atomicMax(&a.key[j], (bid << 16) | (0xFFFFu - (uint32_t)w));
   }
 }
@@ -1715,6 +1731,7 @@ __global__ __launch_bounds__(256) void sa_snapshot_kernel(SegAuction a, int32_t*
     } else {
       a.cost[i] = a.s_cost[i];
       a.hb[i] = a.s_hb[i];
+      if (a.js) a.js[i] = ((uint32_t)(a.s_hb[i] & 0xFFFF) << 16) | a.s_cost[i];
       a.nobid[i] = a.s_nobid[i];
       out[i] = a.s_out[i];
     }
@@ -1840,6 +1857,8 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   a.loff = list ? c.take<int64_t>(nm) : nullptr;
   a.lcs = list ? c.take<int32_t>(nm) : nullptr;
   a.lany = list ? c.take<uint32_t>(1) : nullptr;
+  const char* ej = getenv("RQSID_LIST_JS");  // 0: the list rounds gather winner and cost separately (A/B)
+  a.js = list && K <= 65535 && !(ej && atoi(ej) == 0) ? c.take<uint32_t>(N) : nullptr;
   const char* ls = getenv("RQSID_LIST_START");
   a.lstart = ls ? std::max(1, atoi(ls)) : K >= kListWideK ? kListStartWide : kListStart;
   const char* ed = getenv("RQSID_LIST_DELTA");
