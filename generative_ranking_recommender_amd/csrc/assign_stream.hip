@@ -651,6 +651,11 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
   const float tgy = __uint_as_float(uni(__float_as_uint(trow[3])));
   int* const dummy = p.work_count + 16;                 // sink of the fixed-count stores
   const uint32_t cunits = (!T3 && p.c16h) ? 64u : 128u;  // 16-B units per centre row of the table gathered
+#ifdef RQSID_AB_HALFROW
+  constexpr int kXR = 2;  // row DMA ops per wave and chunk (the probe's 64-B fp16 row pieces)
+#else
+  constexpr int kXR = 4;  // row DMA ops per wave and chunk
+#endif
 
   // ---- header pipeline pieces -------------------------------------------------------------
   // level 1: row indices (wave w: rows 32w..32w+31, lanes 0..31), candidate indices (wave w:
@@ -748,7 +753,15 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
   auto issue_x = [&](const Next& n, int j) __attribute__((always_inline)) {  // this group's rows of chunk j
     const uint32_t sx = lds0 + L::kX + (grp * 3 + (qb + j) % 3) * L::kXG + gw * 4096;
     const char* xb = xbase + (j & 15) * (kSC * 4);
-#ifndef RQSID_AB_NOROWDMA  // (timing probe only: no row traffic, wrong results)
+#if defined(RQSID_AB_HALFROW)  // (timing probe only, wrong results: the DMA of 1-KiB fp16 rows, 64 B per row and chunk)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rr = 16 * i + (lane >> 2);
+      const uint32_t xq = (lane >> 5) ? n.xi[2 * i + 1] : n.xi[2 * i];
+      const uint32_t row = (uint32_t)__shfl((int)(xq >> 7), (rr & 7) * 8);
+      dma16_nt(xbase + (uint64_t)row * 1024u + (j & 15) * 64 + (lane & 3) * 16, uni(sx + i * 1024));
+    }
+#elif !defined(RQSID_AB_NOROWDMA)  // (NOROWDMA: timing probe only, no row traffic, wrong results)
 #pragma unroll
     for (int i = 0; i < 4; ++i) dma16_nt(addr(xb, n.xi[i]), uni(sx + i * 1024));
 #endif
@@ -1023,15 +1036,15 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
       ST(const uint64_t st_w0 = ST_NOW();)
       if (tail) wait_vm<0>();
       else if (grp == 0) {  // rows(j): phase 2j-5; younger: rows(j+1), rows(j+2) [+ E, header]
-        if (!first && j <= 2) wait_vm<8 + L::E>();
-        else if (more && (j == 3 || j == 4)) wait_vm<8 + L::H1>();
-        else if (more && (j == 7 || j == 8)) wait_vm<8 + L::H2>();
-        else wait_vm<8>();
+        if (!first && j <= 2) wait_vm<2 * kXR + L::E>();
+        else if (more && (j == 3 || j == 4)) wait_vm<2 * kXR + L::H1>();
+        else if (more && (j == 7 || j == 8)) wait_vm<2 * kXR + L::H2>();
+        else wait_vm<2 * kXR>();
       } else {  // centres(j): phase 2j-2; younger: rows(j+1) [+ E, header]
-        if (!first && j == 1) wait_vm<4 + L::E>();
-        else if (more && j == 4) wait_vm<4 + L::H1>();
-        else if (more && j == 8) wait_vm<4 + L::H2>();
-        else wait_vm<4>();
+        if (!first && j == 1) wait_vm<kXR + L::E>();
+        else if (more && j == 4) wait_vm<kXR + L::H1>();
+        else if (more && j == 8) wait_vm<kXR + L::H2>();
+        else wait_vm<kXR>();
       }
       lgkm_barrier();
       ST(const uint64_t st_w1 = ST_NOW(); st_wait += st_w1 - st_w0;)
@@ -1052,10 +1065,10 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
       ST(const uint64_t st_w0 = ST_NOW();)
       if (grp == 1) {  // rows(j): phase 2j-4; younger: phases 2j-2, 2j [+ E, header]
         if (tail) wait_vm<0>();
-        else if (!first && j <= 1) wait_vm<2 * (PC + 4) + L::E>();
-        else if (more && (j == 3 || j == 4)) wait_vm<2 * (PC + 4) + L::H1>();
-        else if (more && (j == 7 || j == 8)) wait_vm<2 * (PC + 4) + L::H2>();
-        else wait_vm<2 * (PC + 4)>();
+        else if (!first && j <= 1) wait_vm<2 * (PC + kXR) + L::E>();
+        else if (more && (j == 3 || j == 4)) wait_vm<2 * (PC + kXR) + L::H1>();
+        else if (more && (j == 7 || j == 8)) wait_vm<2 * (PC + kXR) + L::H2>();
+        else wait_vm<2 * (PC + kXR)>();
       }
       lgkm_barrier();
       ST(const uint64_t st_w1 = ST_NOW(); st_wait += st_w1 - st_w0;)
