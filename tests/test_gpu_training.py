@@ -381,7 +381,8 @@ def test_auction_bid_list_equals_sweep(n, k, half, monkeypatch):
     assignment and round count (RQSID_AUCTION_LIST=0) on the level-0 (K = 128) and candidate-fit (K = 1280,
     fp16 cdist) shapes, with the retention (round < 100) and leftover (round > 1000, N % K != 0) rules; above
     8192 jobs per worker (one segment) the default is the multi-block form (sa_mlist_*), checked against the
-    sweep and the one-block form (RQSID_AUCTION_LIST=2); lists are built from round 32 on; times all (printed)."""
+    sweep and the one-block form (RQSID_AUCTION_LIST=2); lists are built from round 32 on; the list rounds gather a
+    packed {winner, cost} word per listed job (RQSID_LIST_JS=0, mode "1s": the two arrays); times all (printed)."""
     import time
     x = synth.small_mixture(n, m=3000, seed=k)
     x /= np.linalg.norm(x, axis=1, keepdims=True)
@@ -389,8 +390,9 @@ def test_auction_bid_list_equals_sweep(n, k, half, monkeypatch):
     c = xg[torch.from_numpy(np.random.default_rng(k).choice(n, k, replace=False)).to(DEV)] * 0.9
     w = ops.auction_scores(xg, c, half=half)
     out = {}
-    for mode in ("1", "0", "2"):
-        monkeypatch.setenv("RQSID_AUCTION_LIST", mode)
+    for mode in ("1", "1s", "0", "2"):
+        monkeypatch.setenv("RQSID_AUCTION_LIST", mode[0])
+        monkeypatch.setenv("RQSID_LIST_JS", "0" if mode == "1s" else "1")  # 1s: winner and cost gathered separately
         ops.auction(w)
         torch.cuda.synchronize()
         t = time.perf_counter()
@@ -400,6 +402,7 @@ def test_auction_bid_list_equals_sweep(n, k, half, monkeypatch):
         out[mode] = (a.cpu().numpy(), rounds)
         print(f"n={n} k={k} list={mode}: {rounds} rounds, {dt * 1e3 / rounds:.3f} ms/round")
     assert np.array_equal(out["1"][0], out["0"][0]) and out["1"][1] == out["0"][1]
+    assert np.array_equal(out["1s"][0], out["0"][0]) and out["1s"][1] == out["0"][1]
     assert np.array_equal(out["2"][0], out["0"][0]) and out["2"][1] == out["0"][1]
     if n % k:
         assert out["1"][1] == 1002
