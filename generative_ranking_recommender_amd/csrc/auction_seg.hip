@@ -1988,7 +1988,8 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   // list-only blocks are longer: their rounds are a few launches each, and the host's readback and launch
   // between two blocks (tens of us) cost as much as several rounds; a failed list replays the block's first
   // kPoll rounds in full from its snapshot, then the loop goes on from there
-  constexpr int kPollList = 32;
+  const char* elb = getenv("RQSID_LIST_BLOCK");  // list-only rounds per captured block (A/B; default 32)
+  const int kPollList = elb ? std::min(256, std::max(kPoll, atoi(elb))) : 32;
   // lean rounds leave out the two-pass kernels of missed workers (five launches of a few us each, empty
   // in most rounds); a lean block runs from a snapshot of the round state and is replayed with the full
   // rounds when any worker missed in it, so the result is the full rounds' in every case
