@@ -2082,15 +2082,27 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   bool try_lean = false;  // round 0 misses everywhere (thresholds start at key 0)
   for (int done = 0; rc == RQSID_OK && (max_rounds <= 0 || done < max_rounds);) {
     int n = max_rounds > 0 ? std::min(kPoll, max_rounds - done) : kPoll;
-    const bool lonly = try_list && exec_list && (max_rounds <= 0 || max_rounds - done >= kPollList);
+    bool lonly = try_list && exec_list && (max_rounds <= 0 || max_rounds - done >= kPollList);
+    // a list-only block must end by round 1000 (the leftover rounds > 1000 bid on unlisted pairs: every list
+    // fails there, and a failed block costs its rounds plus a full replay): the rounds up to 1000 that no
+    // whole block fits run list-only by direct launches (the list tail), from the same snapshot
+    bool ltail = false;
+    if (lonly && done + kPollList > 1001) {
+      lonly = false;
+      ltail = done < 1001 && (max_rounds <= 0 || max_rounds - done >= 1001 - done);
+      if (ltail) n = 1001 - done;
+    }
     if (lonly) n = kPollList;
-    const bool lean = !lonly && try_lean && exec_lean && n == kPoll;
-    (lonly ? n_list : lean ? n_lean : n_full) += 1;
+    const bool lean = !lonly && !ltail && try_lean && exec_lean && n == kPoll;
+    (lonly || ltail ? n_list : lean ? n_lean : n_full) += 1;
     if (fill_async(a.live_count + 2, 0, 8, st) != hipSuccess) {
       rc = fail(RQSID_E_LAUNCH, "seg_auction: memset");
       break;
     }
-    if (lonly || lean) {
+    if (ltail) {
+      hipLaunchKernelGGL(sa_snapshot_kernel, dim3(gsnap), dim3(256), 0, st, a, out_assign, n_jobs, 0);
+      for (int i = 0; i < n; ++i) launch_round(st, i == n - 1, true, true);
+    } else if (lonly || lean) {
       hipLaunchKernelGGL(sa_snapshot_kernel, dim3(gsnap), dim3(256), 0, st, a, out_assign, n_jobs, 0);
       if (hipGraphLaunch(lonly ? exec_list : exec_lean, st) != hipSuccess) {
         rc = fail(RQSID_E_LAUNCH, "seg_auction: graph launch");
@@ -2110,7 +2122,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
       rc = fail(RQSID_E_LAUNCH, "seg_auction: readback");
       break;
     }
-    if ((lean && host[2]) || (lonly && host[3])) {
+    if ((lean && host[2]) || ((lonly || ltail) && host[3])) {
       // a worker missed inside the lean block, or a list failed inside the list-only block: back to its
       // start, replay it with the exact passes
       hipLaunchKernelGGL(sa_snapshot_kernel, dim3(gsnap), dim3(256), 0, st, a, out_assign, n_jobs, 1);
@@ -2130,7 +2142,8 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
       n = kPoll;  // the replayed block's rounds (a list-only block's later rounds are not run)
     } else {
       try_lean = n_multi > 0;
-      try_list = host[3] == 0;  // every list held through this block
+      // every list held through this block, and the block's sweep rounds reached the list start (lists exist)
+      try_list = host[3] == 0 && done + n > a.lstart;
     }
     done += n;
     if (host[0] == 0) break;
