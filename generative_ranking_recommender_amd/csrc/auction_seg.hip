@@ -1324,7 +1324,10 @@ __global__ __launch_bounds__(256) RQ_BID_ATTR void sa_bid_kernel(SegAuction a) {
 // bid eps); bids, retention / leftover overrides and the packed atomicMax of the sweep.
 constexpr int kListEq = 2048;  // values equal to T a list round ranks in LDS (more: sweep)
 constexpr int kLT = 1024;  // threads of a list-round block
-__global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
+// LT threads per block: 1024, or 256 when every list is short (the middle layer's lockstep sub-fits: 128
+// segments x 128 workers, lists of ~500 entries, 16384 blocks per round)
+template <int LT>
+__global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
   const int64_t hw = blockIdx.x;
   const int r = (int)(hw / a.K), w = (int)(hw % a.K);
   const int sg = a.mseg[r];
@@ -1355,7 +1358,7 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
   __syncthreads();
   // pass 1: this round's value keys (raw score, cost, last winner), kept in the entries' upper 16 bits so
   // the later passes read the list only
-  for (uint32_t i = tid; i < n; i += kLT) {
+  for (uint32_t i = tid; i < n; i += LT) {
     const uint2 e = L[i];
     const uint32_t k = okey(value_bits(w, (uint16_t)e.y, js_hb(a, e.x), js_cost(a, e.x)));
     L[i].y = (e.y & 0xFFFFu) | (k << 16);
@@ -1381,7 +1384,7 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
   __syncthreads();
   if (tid < 256) hst[tid] = 0;
   __syncthreads();
-  for (uint32_t i = tid; i < n; i += kLT) {
+  for (uint32_t i = tid; i < n; i += LT) {
     const uint32_t k = L[i].y >> 16;
     if (k >= kb && (k >> 8) == b1) atomicAdd(&hst[k & 255u], 1u);
   }
@@ -1409,7 +1412,7 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
       __syncthreads();
       if (tid < 256) hst[tid] = 0;
       __syncthreads();
-      for (uint32_t i = tid; i < n; i += kLT) {
+      for (uint32_t i = tid; i < n; i += LT) {
         const uint2 e = L[i];
         if ((e.y >> 16) == T && (shift == 24 || (e.x >> (shift + 8)) == J))
           atomicAdd(&hst[(e.x >> shift) & 255u], 1u);
@@ -1446,7 +1449,7 @@ __global__ __launch_bounds__(kLT) void sa_list_round_kernel(SegAuction a) {
   const _Float16 epsh = __builtin_bit_cast(_Float16, eps);
   const _Float16 vT = __builtin_bit_cast(_Float16, okey_inv(T));
   const bool ret = counter < 100;
-  for (uint32_t i = tid; i < n; i += kLT) {
+  for (uint32_t i = tid; i < n; i += LT) {
     const uint2 e = L[i];
     const uint32_t j = e.x, k = e.y >> 16;
     uint32_t bid = 0;
@@ -1759,7 +1762,8 @@ __global__ __launch_bounds__(256) void sa_snapshot_kernel(SegAuction a, int32_t*
     for (int64_t hw = g0; hw < (int64_t)a.n_multi * a.K; hw += gs) a.lcnt[hw * kAbovePad] = 0;
 }
 
-// multi-chunk segment ranks (one block): hidx[s] = rank or -1, mseg[rank] = s; live_count[1] = total
+// multi-chunk segment ranks (one block): hidx[s] = rank or -1, mseg[rank] = s; live_count[1] = total,
+// live_count[2] = the most jobs in one of them
 __global__ __launch_bounds__(1024) void sa_multi_index_kernel(SegAuction a) {
   __shared__ uint32_t ws[16];
   __shared__ uint32_t carry;
@@ -1779,6 +1783,7 @@ __global__ __launch_bounds__(1024) void sa_multi_index_kernel(SegAuction a) {
       const uint32_t r = off + before;
       a.hidx[s] = v ? (int32_t)r : -1;
       if (v && (int32_t)r < a.n_multi) a.mseg[r] = s;
+      if (v) atomicMax(&a.live_count[2], (uint32_t)(a.seg_off[s + 1] - a.seg_off[s]));  // the longest (list size)
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1951,7 +1956,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   hipLaunchKernelGGL(sa_seg_init_kernel, dim3(gs), dim3(256), 0, st, a, active);
   hipLaunchKernelGGL(sa_multi_index_kernel, dim3(1), dim3(1024), 0, st, a);
   if ((rc = check_launch("seg_auction_init")) ||
-      hipMemcpyAsync(host, a.live_count, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(host, a.live_count, 12, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return rc ? rc : fail(RQSID_E_LAUNCH, "seg_auction: init readback");
   if ((int32_t)host[1] != n_multi)
@@ -2008,6 +2013,9 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   // over 6.25M jobs.  Such a block runs from a snapshot like a lean block and is replayed in full when any
   // list failed in it (live_count[3]).
   const bool list_only_ok = a.lst && !any_single;
+  // short lists (<= 4096 entries of capacity in every segment) take 256-thread list-round blocks
+  const char* els = getenv("RQSID_LIST_SMALL");  // 0: always 1024 threads (A/B)
+  const bool lsmall = 4 * ((int64_t)host[2] / n_workers) + 256 <= 4096 && !(els && atoi(els) == 0);
   auto launch_round = [&](hipStream_t q, bool count, bool lean, bool list_only = false) {
     if (a.lst && a.lmb_chunks) {
       const dim3 gw((unsigned)(n_multi * a.K)), gp((unsigned)((int64_t)n_multi * a.K * a.lmb_chunks));
@@ -2020,7 +2028,8 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
       hipLaunchKernelGGL(sa_mlist_eq_kernel, gw, dim3(kLT), 0, q, a);
       hipLaunchKernelGGL(sa_mlist_pass_kernel<3>, gp, dim3(256), 0, q, a);
     } else if (a.lst) {
-      hipLaunchKernelGGL(sa_list_round_kernel, dim3((unsigned)(n_multi * a.K)), dim3(kLT), 0, q, a);
+      if (lsmall) hipLaunchKernelGGL(sa_list_round_kernel<256>, dim3((unsigned)(n_multi * a.K)), dim3(256), 0, q, a);
+      else hipLaunchKernelGGL(sa_list_round_kernel<kLT>, dim3((unsigned)(n_multi * a.K)), dim3(kLT), 0, q, a);
     }
     SegAuction ar = a;
     ar.rcount = count ? 1 : 0;
