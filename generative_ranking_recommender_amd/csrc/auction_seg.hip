@@ -2013,9 +2013,13 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   // over 6.25M jobs.  Such a block runs from a snapshot like a lean block and is replayed in full when any
   // list failed in it (live_count[3]).
   const bool list_only_ok = a.lst && !any_single;
-  // short lists (<= 4096 entries of capacity in every segment) take 256-thread list-round blocks
-  const char* els = getenv("RQSID_LIST_SMALL");  // 0: always 1024 threads (A/B)
-  const bool lsmall = 4 * ((int64_t)host[2] / n_workers) + 256 <= 4096 && !(els && atoi(els) == 0);
+  // short lists take 256-thread list-round blocks: capacity <= 4096 entries in every segment when there are
+  // many segments (S x K blocks per round), <= 1024 for one segment (a 100k x 128 auction, capacity 3380, ran
+  // 0.0194 -> 0.0207 ms per round with 256 threads; K=1280 x 100k, capacity 568, 0.0295 -> 0.0253)
+  const char* els = getenv("RQSID_LIST_SMALL");  // 0: always 1024 threads; n > 1: one capacity limit (A/B)
+  const int64_t lcap_max = 4 * ((int64_t)host[2] / n_workers) + 256;
+  const int64_t lsmall_cap = els && atoi(els) > 1 ? atoi(els) : (n_multi > 1 ? 4096 : 1024);
+  const bool lsmall = lcap_max <= lsmall_cap && !(els && atoi(els) == 0);
   auto launch_round = [&](hipStream_t q, bool count, bool lean, bool list_only = false) {
     if (a.lst && a.lmb_chunks) {
       const dim3 gw((unsigned)(n_multi * a.K)), gp((unsigned)((int64_t)n_multi * a.K * a.lmb_chunks));
