@@ -1847,7 +1847,9 @@ void carve(SegAuction& a, Carve& c, int64_t N, int32_t K, int32_t S, int64_t tot
   const int lmode = el ? atoi(el) : 1;  // 0: sweep only; 1: lists (default); 2: one-block lists at any size
   // one wide segment with long lists: the multi-block list rounds (any jobs per worker); otherwise one block
   // per worker while the lists are short
-  const bool mb = guess && a.n_multi == 1 && lmode == 1 && N / K > kListBlockJpw;
+  const char* emb = getenv("RQSID_LIST_MB_JPW");  // (A/B) the jobs per worker above which lists go multi-block
+  const int64_t mb_jpw = emb ? std::max<int64_t>(1, atoll(emb)) : kListBlockJpw;
+  const bool mb = guess && a.n_multi == 1 && lmode == 1 && N / K > mb_jpw;
   const bool list = guess && a.n_multi > 0 && lmode != 0 && (lmode == 2 || mb || N / (nm * K) <= kListMaxJpw);
   a.lmb_chunks = mb ? (int32_t)((4 * (N / K) + 256 + kMCH - 1) / kMCH) : 0;
   a.lh = mb ? c.take<uint32_t>(nm * K * 512) : nullptr;
