@@ -150,7 +150,7 @@ constexpr int kListStart = 32;
 constexpr int kListStartWide = 16;
 constexpr int kListWideK = 1024;
 constexpr int kMCH = 2048;               // list entries per block of a multi-block list round
-constexpr int kListDelta = 64;   // default keys below last round's threshold kept in the bid list
+constexpr int kListDelta = 32;   // default keys below last round's threshold kept in the bid list (64 measured the same or slower: DESIGN 3.3)
 
 __device__ __forceinline__ int seg_of(const int32_t* __restrict__ off, int n_seg, int64_t i) {
   int lo = 0, hi = n_seg - 1;  // last s with off[s] <= i
