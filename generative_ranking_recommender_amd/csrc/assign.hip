@@ -1351,6 +1351,35 @@ __global__ __launch_bounds__(64) void mfma_probe_kernel(const uint16_t* __restri
   for (int v = 0; v < 16; ++v) d[((v & 3) + 8 * (v >> 2) + 4 * hh) * 32 + i] = acc[v];
 }
 
+// fp8 (OCP e4m3) form, groundwork for a level-1 correction MFMA: D = A.B + C with ONE
+// v_mfma_scale_f32_32x32x64_f8f6f4 (unit scales), A 32x64 and B 64x32 as bytes.  Lane half hh holds K = 32 hh ..
+// 32 hh + 31 of its row (A) / column (B); a dot product is invariant to any K order applied to both operands
+// alike, so A.B + C comes out exactly iff the instruction maps the two operands' registers to K the same way.
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+__global__ __launch_bounds__(64) void mfma_probe_f8_kernel(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
+                                                           const float* __restrict__ c, float* __restrict__ d) {
+  const int l = threadIdx.x, i = l & 31, hh = l >> 5;
+  f32x16 acc;
+#pragma unroll
+  for (int v = 0; v < 16; ++v) acc[v] = c[((v & 3) + 8 * (v >> 2) + 4 * hh) * 32 + i];
+  i32x8 av, bv;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t wa = 0, wb = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = 32 * hh + 4 * j + q;
+      wa |= (uint32_t)a[i * 64 + k] << (8 * q);
+      wb |= (uint32_t)b[k * 32 + i] << (8 * q);
+    }
+    av[j] = (int)wa;
+    bv[j] = (int)wb;
+  }
+  acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av, bv, acc, 0, 0, 0, 127, 0, 127);
+#pragma unroll
+  for (int v = 0; v < 16; ++v) d[((v & 3) + 8 * (v >> 2) + 4 * hh) * 32 + i] = acc[v];
+}
+
 // the hi terms of the interleaved table, contiguous per centre: each 32-dim chunk of c16 is 4 16-B pieces of hi
 // terms then 4 of lo terms, so hi piece i is c16 piece 8 (i / 4) + i % 4
 __global__ __launch_bounds__(256) void centers_hi_kernel(const uint4* __restrict__ c16, int64_t n, uint4* __restrict__ hi) {
@@ -1675,7 +1704,10 @@ int rqsid_debug_stamps_tile(unsigned long long* out8) {
 
 int rqsid_mfma_probe(int32_t f16, const uint16_t* a, const uint16_t* b, const float* c, float* d, void* stream) {
   if (!a || !b || !c || !d) return fail(RQSID_E_ARG, "mfma_probe: null argument");
-  if (f16) hipLaunchKernelGGL(mfma_probe_kernel<true>, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, c, d);
+  if (f16 == 2)
+    hipLaunchKernelGGL(mfma_probe_f8_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uint8_t*>(a), reinterpret_cast<const uint8_t*>(b), c, d);
+  else if (f16) hipLaunchKernelGGL(mfma_probe_kernel<true>, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, c, d);
   else hipLaunchKernelGGL(mfma_probe_kernel<false>, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, c, d);
   return check_launch("mfma_probe");
 }

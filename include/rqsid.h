@@ -300,9 +300,11 @@ int rqsid_dauction_end_round(const uint16_t* scores, int32_t n_workers, int64_t 
 int rqsid_greedy_match(const float* dist, const int32_t* sub_off, int32_t groups, int32_t n_cand,
                        int32_t max_take, uint8_t* match, int32_t* n_selected, void* stream);
 
-/* Numerics probe (self-test): d = a.b + c with ONE v_mfma_f32_32x32x16_f16 (f16 != 0) or
- * _bf16; a [32][16], b [16][32] (half / bfloat16 bits), c/d fp32 [32][32], row-major.  The tests
- * use it to pin the MFMA accumulation model behind rqsid_assign's screening bound. */
+/* Numerics probe (self-test): d = a.b + c with ONE v_mfma_f32_32x32x16_f16 (f16 == 1) or
+ * _bf16 (f16 == 0); a [32][16], b [16][32] (half / bfloat16 bits), c/d fp32 [32][32], row-major.  The tests
+ * use it to pin the MFMA accumulation model behind rqsid_assign's screening bound.  f16 == 2: ONE
+ * v_mfma_scale_f32_32x32x64_f8f6f4 on OCP fp8 e4m3 bytes with unit scales, a [32][64], b [64][32] (the
+ * pointers then address bytes). */
 int rqsid_mfma_probe(int32_t f16, const uint16_t* a, const uint16_t* b, const float* c, float* d,
                      void* stream);
 

@@ -110,3 +110,38 @@ def test_f16_denormals_are_kept():
     assert d[0, 0] == 2.0 ** -10
     assert d[1, 1] == 2.0 ** -48
     assert d[2, 2] == (2.0 ** -15 + 2.0 ** -24) * 8
+
+
+def e4m3_bits(x):
+    """OCP fp8 e4m3 bits of values exactly representable in it (small integers and halves here)."""
+    out = np.zeros(np.shape(x), np.uint8)
+    for idx, v in np.ndenumerate(np.asarray(x, np.float64)):
+        if v == 0:
+            continue
+        sgn = 0x80 if v < 0 else 0
+        m, e = np.frexp(abs(v))          # abs(v) = m 2^e, m in [0.5, 1)
+        E = int(e) - 1 + 7               # biased exponent of 1.f form
+        frac = m * 2 - 1                 # in [0, 1)
+        f3 = int(round(frac * 8))
+        assert 1 <= E <= 15 and f3 * 1.0 == frac * 8 and not (E == 15 and f3 == 7), v
+        out[idx] = sgn | (E << 3) | f3
+    return out
+
+
+def test_fp8_layout_matches_matmul():
+    """ONE v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3, unit scales) on small exact values reproduces A.B + C
+    exactly with the same lane-half -> K placement for both operands (the groundwork a level-1
+    fp8 correction MFMA needs; the instruction's own accumulation model is not pinned yet)."""
+    rng = np.random.default_rng(3)
+    a = rng.integers(-8, 9, (32, 64)).astype(np.float64) / 2.0
+    b = rng.integers(-8, 9, (64, 32)).astype(np.float64) / 2.0
+    c = rng.integers(-100, 100, (32, 32)).astype(np.float32)
+    lib = _lib.load()
+    ta = torch.from_numpy(e4m3_bits(a)).to(DEV)
+    tb = torch.from_numpy(e4m3_bits(b)).to(DEV)
+    tc = torch.from_numpy(c).to(DEV)
+    td = torch.empty((32, 32), dtype=torch.float32, device=DEV)
+    _lib.check(lib.rqsid_mfma_probe(2, ta.data_ptr(), tb.data_ptr(), tc.data_ptr(), td.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream), "probe")
+    torch.cuda.synchronize()
+    assert np.array_equal(td.cpu().numpy(), (a @ b + c).astype(np.float32))
