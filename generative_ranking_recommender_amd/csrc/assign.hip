@@ -1509,12 +1509,12 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
                  float* den_out, int32_t* out_local, int32_t* out_global, int32_t screen_terms, void* workspace,
                  int64_t workspace_bytes, void* stream) {
   if (dim <= 0 || dim % kChunk || dim > kMaxDim || n_rows < 0 || n_segments <= 0 || !seg_row_off ||
-      !seg_tile_off || !centers || !c16 || !c_meta || !cand_base || !cand_count || !out_local || !out_global ||
+      !seg_tile_off || !centers || !c16 || !c_meta || !cand_base || !cand_count || (n_rows > 0 && (!out_local || !out_global)) ||
       n_centers <= 0 || cand_count_max < 0 || max_tiles < 0 || n_rows > INT32_MAX || res_levels < 0 ||
       res_levels > 2 || (screen_terms != 0 && screen_terms != 1 && screen_terms != 3))
     return fail(RQSID_E_ARG, "assign: bad arguments (n=%lld dim=%d S=%d K=%d levels=%d)", (long long)n_rows, dim,
                 n_segments, n_centers, res_levels);
-  if ((res_levels >= 1 && !ca) || (res_levels == 2 && (!cb || !seg_cb || (res_normalize && !den_in))))
+  if ((res_levels >= 1 && !ca) || (res_levels == 2 && (!cb || !seg_cb || (res_normalize && n_rows > 0 && !den_in))))
     return fail(RQSID_E_ARG, "assign: residual inputs missing for res_levels=%d", res_levels);
   if (!workspace || workspace_bytes < rqsid_assign_workspace_bytes(n_rows))
     return fail(RQSID_E_WORKSPACE, "assign: workspace too small");

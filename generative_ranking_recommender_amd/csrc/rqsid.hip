@@ -615,7 +615,7 @@ int rqsid_bucket(const int32_t* keys, int64_t n, int32_t S, int32_t tile_rows, i
 int rqsid_residual(const float* x, int64_t n, int32_t dim, const float* centers, int32_t n_centers,
                    const int32_t* center_id, const int32_t* group_dims, int32_t n_groups, int32_t normalize,
                    float* out, void* stream) {
-  if (!x || !centers || !center_id || !out || dim <= 0 || dim % 4 || n < 0 || n_centers <= 0 ||
+  if ((n > 0 && (!x || !center_id || !out)) || !centers || dim <= 0 || dim % 4 || n < 0 || n_centers <= 0 ||
       (normalize && (!group_dims || n_groups <= 0 || n_groups > kMaxGroups)))
     return fail(RQSID_E_ARG, "residual: bad arguments (dim=%d groups=%d)", dim, n_groups);
   if (n == 0) return RQSID_OK;
@@ -626,7 +626,7 @@ int rqsid_residual(const float* x, int64_t n, int32_t dim, const float* centers,
 
 int rqsid_scale_groups(const float* x, int64_t n, int32_t dim, const int32_t* group_dims, int32_t n_groups,
                        const float* weights, float* out, void* stream) {
-  if (!x || !group_dims || !weights || !out || n_groups <= 0 || dim <= 0 || n < 0)
+  if ((n > 0 && (!x || !out)) || !group_dims || !weights || n_groups <= 0 || dim <= 0 || n < 0)
     return fail(RQSID_E_ARG, "scale_groups: bad arguments");
   if (n == 0) return RQSID_OK;
   hipLaunchKernelGGL(scale_groups_kernel, dim3(grid_cap(cdiv(n * dim, 256 * 8), 8192)), dim3(256), 0,
@@ -682,7 +682,7 @@ int rqsid_match_to_candidates(const uint8_t* match, int32_t groups, int32_t n_ca
 
 int rqsid_pairwise_distance(const float* x, int64_t n, int32_t dim, const float* centers, int32_t k, float* out,
                             void* stream) {
-  if (!x || !centers || !out || n < 0 || k <= 0 || dim <= 0 || dim % 32)
+  if ((n > 0 && (!x || !out)) || !centers || n < 0 || k <= 0 || dim <= 0 || dim % 32)
     return fail(RQSID_E_ARG, "pairwise_distance: bad arguments");
   if (n == 0) return RQSID_OK;
   hipLaunchKernelGGL(pairwise_distance_kernel<0>, dim3((unsigned)cdiv(n, kPdTile), (unsigned)cdiv(k, kPdTile)),
@@ -692,7 +692,7 @@ int rqsid_pairwise_distance(const float* x, int64_t n, int32_t dim, const float*
 
 int rqsid_pairwise_cosine(const float* x, int64_t n, int32_t dim, const float* centers, int32_t k, float* out,
                           uint16_t* out_wj, void* stream) {
-  if (!x || !centers || (!out && !out_wj) || n < 0 || k <= 0 || dim <= 0 || dim % 32)
+  if ((n > 0 && (!x || (!out && !out_wj))) || !centers || n < 0 || k <= 0 || dim <= 0 || dim % 32)
     return fail(RQSID_E_ARG, "pairwise_cosine: bad arguments");
   if (n == 0) return RQSID_OK;
   hipLaunchKernelGGL(pairwise_distance_kernel<3>, dim3((unsigned)cdiv(n, kPdTile), (unsigned)cdiv(k, kPdTile)),
@@ -702,7 +702,7 @@ int rqsid_pairwise_cosine(const float* x, int64_t n, int32_t dim, const float* c
 
 int rqsid_auction_scores(const float* x, int64_t n, int32_t dim, const float* centers, int32_t k, int32_t half,
                          uint16_t* out_wj, void* stream) {
-  if (!x || !centers || !out_wj || n < 0 || k <= 0 || dim <= 0 || dim % 32)
+  if ((n > 0 && (!x || !out_wj)) || !centers || n < 0 || k <= 0 || dim <= 0 || dim % 32)
     return fail(RQSID_E_ARG, "auction_scores: bad arguments");
   if (n == 0) return RQSID_OK;
   const dim3 g((unsigned)cdiv(n, kPdTile), (unsigned)cdiv(k, kPdTile));
@@ -718,7 +718,7 @@ int rqsid_auction_scores(const float* x, int64_t n, int32_t dim, const float* ce
 int rqsid_seg_auction_scores(const float* x, int64_t n, int32_t dim, const float* centers, int32_t k,
                              int32_t n_seg, const int32_t* seg_off, const int32_t* seg_tile_off, int64_t n_tiles,
                              int32_t half, uint16_t* out_wj, void* stream) {
-  if (!x || !centers || !out_wj || !seg_off || !seg_tile_off || n < 0 || k <= 0 || dim <= 0 || dim % 32 ||
+  if ((n > 0 && (!x || !out_wj)) || !centers || !seg_off || !seg_tile_off || n < 0 || k <= 0 || dim <= 0 || dim % 32 ||
       n_seg <= 0 || n_tiles < 0 || n_tiles > INT32_MAX)
     return fail(RQSID_E_ARG, "seg_auction_scores: bad arguments");
   if (n == 0 || n_tiles == 0) return RQSID_OK;

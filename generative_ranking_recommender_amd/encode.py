@@ -126,6 +126,9 @@ class RQEncoder:
             raise IndexError("list index out of range")  # reference: all_cluster_ids[-2] with one level
         n = x.shape[0]
         out = torch.empty((self.L, n), dtype=torch.int32, device=x.device)
+        if n == 0:
+            self.last_rescored = []
+            return out.t()
         ws = self._workspace(n)
         self.last_rescored = []
         if self.fused:

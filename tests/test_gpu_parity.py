@@ -299,6 +299,30 @@ def test_encoder_full_size_properties():
     assert (an[sel] == ref).all()
 
 
+@pytest.mark.parametrize("n", [0, 1, 2, 127, 128, 129, 255, 256, 257, 1023, 4097])
+def test_encoder_empty_and_ragged_batches(n):
+    """Batch sizes around the 128-row (levels 0/1) and 256-row (level 2 ping-pong) tile edges, one row and
+    no rows, at PROD codebook shapes: every row's IDs equal the exact oracle's, in both the training and the
+    reference-predict semantics; an empty batch gives an empty [0, 3] result."""
+    cb = synth.encode_codebooks(seed=99)
+    cents = [torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")]
+    x = synth.mixture_rows(5, 5 + n) if n else np.zeros((0, 512), np.float32)
+    for sem, weighted in ((HIERARCHICAL_TRAIN, True), (HIERARCHICAL_PREDICT_REFERENCE, None)):
+        got = RQEncoder(cents, [128, 128, 256], match=torch.from_numpy(cb["match"]), semantics=sem,
+                        device=DEV).encode(gpu(x)).cpu().numpy()
+        assert got.shape == (n, 3)
+        if not n:
+            assert ops.nearest(gpu(x), ops.prepare_centers(gpu(cb["c0"]))).shape == (0,)
+        if n and weighted:
+            ref = O.encode(x, [cb["c0"], cb["c1"], cb["c2"]], [128, 128, 256], cb["match"],
+                           residual_from_weighted=True, exact=True)
+            assert (got == ref).all()
+        if n:
+            full = RQEncoder(cents, [128, 128, 256], match=torch.from_numpy(cb["match"]), semantics=sem,
+                             device=DEV).encode(gpu(synth.mixture_rows(5, 5005))).cpu().numpy()
+            assert (got == full[:n]).all()  # a row's IDs do not depend on the batch it is encoded in
+
+
 def test_encoder_xl_shapes_properties():
     """BASELINE configs[4] shapes (need [256,256,512], 5120 last-level candidates, 65536 groups): the
     middle level screens 256 candidates per parent (1-term), the last level 512 per group (multi-pass
