@@ -92,7 +92,7 @@ def parse():
 LEVEL_KERNELS = {
     "prod": {0: ("assign_screen_kernel<4, 2, 0, false, false, true, 1>", "assign_rescore_half_kernel<0, false>"),
              1: ("assign_screen_kernel<4, 2, 1, true, true, true, 1>", "assign_rescore_half_kernel<1, true>"),
-             2: ("assign_pp_kernel<8, 2, true, false>", "assign_rescore_half_kernel<2, true>")},
+             2: ("assign_pc_kernel<8, 2, true, false>", "assign_rescore_half_kernel<2, true>")},
     # [256,256,512]: 256-candidate level 0 (per-tile form); 256-candidate 3-term level 1 in one pass
     # (candidate-split screen, CW = 2); 512-candidate level 2 on the row-resident screen (assign_rows.hip)
     "xl": {0: ("assign_screen_kernel<8, 2, 0, false, false, true, 1>", "assign_rescore_half_kernel<0, false>"),
@@ -263,6 +263,78 @@ def cpu_baseline(cb, rows):
     return {"value": rows / dt, "unit": "vectors/s", "cores": int(threads), "kind": "port",
             "sample": f"{rows} rows x 3 levels, oracle/rq_oracle.py encode (numpy fp32 BLAS, {threads} threads), "
                       f"{dt:.2f} s"}
+
+
+def _gpu_seconds(fn, reps=3):
+    """Mean wall seconds of fn() on the device (synchronised), after one warm-up call."""
+    fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / reps
+
+
+def cpu_baselines_8d(cb, dev):
+    """SURVEY §8(d)'s CPU-baseline set beside the same unit on the GPU, on the same rows (rank 0, N=1):
+    single-level assign (K=128) at 100k and 1M rows, one Lloyd iteration (assign + centroid update) at 1M rows,
+    one balanced-auction round at 100,001 x 128 (N % K != 0, as a 1002-round level-0 fit runs).  CPU: the
+    oracle's restatements of the reference (balancekmeans/__init__.py:489-534 predict, :315-324 update,
+    :12-140 auction with torch CPU ops); GPU: the librqsid path each replaces.  Bounded: ~10 s of CPU work."""
+    from threadpoolctl import threadpool_info
+    from oracle import rq_oracle as O
+    threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    c0 = cb["c0"]
+    c0d = torch.from_numpy(c0).to(dev)
+    pc0 = ops.prepare_centers(c0d)
+    out = {"cores": int(threads), "torch_threads": int(torch.get_num_threads()), "kind": "port",
+           "note": "cpu: oracle/rq_oracle.py (numpy fp32 BLAS / torch CPU ops); gpu: librqsid on the same rows"}
+    x1m = synth.mixture_rows(0, 1_000_000)
+    for rows in (100_000, 1_000_000):
+        xs = x1m[:rows]
+        t = time.perf_counter()
+        O.nearest(xs, c0)
+        cpu = time.perf_counter() - t
+        xd = torch.from_numpy(xs).to(dev)
+        gpu = _gpu_seconds(lambda: ops.nearest(xd, pc0))
+        out[f"assign_k128_{rows // 1000}k"] = {
+            "unit": "rows/s", "cpu": round(rows / cpu, 1), "gpu": round(rows / gpu, 1),
+            "cpu_s": round(cpu, 3), "gpu_ms": round(gpu * 1e3, 3),
+            "reference": "balancekmeans/__init__.py:489-534 (pairwise_distance_full + argmin)"}
+    # one Lloyd iteration (unbalanced KMeans.fit step) at 1M rows
+    t = time.perf_counter()
+    a = O.nearest(x1m, c0)
+    O.centroid_update(x1m, a, c0, lambda n: 0)
+    cpu = time.perf_counter() - t
+    xd = torch.from_numpy(x1m).to(dev)
+
+    def lloyd():
+        ids = ops.nearest(xd, ops.prepare_centers(c0d))
+        ops.centroid_update(xd, ids, c0.shape[0], c0d.clone())
+    gpu = _gpu_seconds(lloyd)
+    out["lloyd_iteration_1m"] = {"unit": "rows/s", "cpu": round(1e6 / cpu, 1), "gpu": round(1e6 / gpu, 1),
+                                 "cpu_s": round(cpu, 3), "gpu_ms": round(gpu * 1e3, 3),
+                                 "reference": "balancekmeans/__init__.py:368-465 (one fit iteration: predict + :315-324)"}
+    # one balanced-auction round at 100,001 jobs x 128 workers
+    n_a = 100_001
+    d = O.cdist_f32(x1m[:n_a], c0)
+    rounds_cpu = 5
+    cpu_round = O.auction_rounds_torch_cpu(-d, rounds_cpu)
+    w = torch.from_numpy(np.ascontiguousarray((-d).T)).to(dev).half().contiguous()
+    ops.auction(w)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    _, r = ops.auction(w)
+    torch.cuda.synchronize()
+    g = time.perf_counter() - t
+    rounds = int(r) if not isinstance(r, torch.Tensor) else int(r.max().item())
+    out["auction_round_100k"] = {"unit": "ms per round", "cpu": round(cpu_round * 1e3, 3),
+                                 "gpu": round(g / max(rounds, 1) * 1e3, 4),
+                                 "sample": f"{n_a} x 128 fp16 scores; cpu: {rounds_cpu} rounds of the reference's "
+                                           f"torch CPU ops; gpu: the whole auction ({rounds} rounds) / rounds",
+                                 "reference": "balancekmeans/__init__.py:12-140 (auction_lap_half)"}
+    return out
 
 
 def config0(dev, rows=100_000, cpu_rounds=40):
@@ -627,6 +699,10 @@ def main():
         line["parity"] = check_sample(x, out, cb, args.parity_rows)
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_sample > 0:
         line["cpu_baseline"] = cpu_baseline(cb, args.cpu_sample)
+        try:
+            line["cpu_baselines_8d"] = cpu_baselines_8d(cb, dev)
+        except Exception as exc:  # a side measurement must not cost the encode line
+            line["cpu_baselines_8d"] = {"error": repr(exc)[:300]}
     if rank == 0 and world == 1 and args.config0:
         try:
             line["config0"] = config0(dev)

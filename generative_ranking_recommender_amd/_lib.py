@@ -19,7 +19,8 @@ PKG = Path(__file__).resolve().parent
 REPO = PKG.parent
 LIB_PATH = PKG / "librqsid.so"
 SRCS = [PKG / "csrc" / "rqsid.hip", PKG / "csrc" / "assign.hip", PKG / "csrc" / "assign_stream.hip",
-        PKG / "csrc" / "assign_resident.hip", PKG / "csrc" / "assign_rows.hip", PKG / "csrc" / "auction.hip",
+        PKG / "csrc" / "assign_resident.hip", PKG / "csrc" / "assign_rows.hip", PKG / "csrc" / "assign_pc.hip",
+        PKG / "csrc" / "auction.hip",
         PKG / "csrc" / "auction_seg.hip"]
 DEPS = SRCS + [PKG / "csrc" / "internal.h", PKG / "csrc" / "assign_common.h"]
 HEADER = REPO / "include" / "rqsid.h"
@@ -37,6 +38,7 @@ c_i32, c_i64, c_f32, c_vp, c_char_p = ctypes.c_int32, ctypes.c_int64, ctypes.c_f
 SIGNATURES = {
     "rqsid_version": (c_i32, []),
     "rqsid_last_error": (c_char_p, []),
+    "rqsid_build_flags": (c_i32, []),
     "rqsid_prepare_centers": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp]),
     "rqsid_prepare_centers_hi": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
     "rqsid_bucket_workspace_bytes": (c_i64, [c_i64, c_i32]),
@@ -192,6 +194,12 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    flags = int(lib.rqsid_build_flags())
+    if flags and "RQSID_LIB" not in os.environ:
+        # a timing-probe build (tools/ab_build.sh) returns wrong IDs by design: only an explicit RQSID_LIB A/B
+        # run may load one
+        raise RuntimeError(f"{path} is a timing-probe build (rqsid_build_flags = {flags}); rebuild with "
+                           "`python -c 'import __graft_entry__ as g; g.build()'`")
     _lib = lib
     return lib
 

@@ -914,8 +914,8 @@ __device__ __forceinline__ double half_sum(double v) {
 // consecutive items are rows of one segment walking the same candidates, so a candidate row is read from
 // L2 once per block rather than once per row (the per-row arithmetic is the same code)
 constexpr int kOvfSlot = 56;  // workspace header int: overflow item count
-// workspace header int 60: error word of the counter-driven list writes (zeroed with the header by every
-// rqsid_assign call, read by rqsid_assign_error).  Each index such a write takes from a device counter is
+// workspace header int 60: sticky error word of the counter-driven list writes (NOT cleared by a call: the
+// caller zeroes it when it allocates the workspace; ops.AssignWorkspace.error() / RQEncoder.errors() read it).  Each index such a write takes from a device counter is
 // checked against its slot's capacity; a write that would fall outside is dropped and its bit raised, so
 // a wrong count can only produce a reported error, never a store outside the workspace.
 constexpr int kErrSlot = 60;
@@ -1601,7 +1601,26 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   // keeps the ping-pong form (7.4 vs 7.6-7.8 ms)
   const bool use_rows = (variant == 8 || (variant == 0 && res_levels >= 1 && cand_count_max > 256)) &&
                         rows_supported(dim, cand_count_max, t3, res_levels, norm) && (int64_t)n_segments + 1 <= n_rows;
-  if (use_rows) {
+  // the producer/consumer screen (assign_pc.hip): the default for the residual levels it covers (PROD level 1,
+  // 3-term <= 128 candidates, and level 2, 1-term <= 256); RQSID_PC=0 keeps the older
+  // dispatch above for A/B, variant 9 forces it wherever it applies
+  const char* pce = getenv("RQSID_PC");
+  const bool pc_ok = pc_supported(dim, cand_count_max, t3, res_levels) && !cand_lid &&
+                     (res_levels != 1 || !norm || den_out) && (int64_t)n_segments + 1 <= n_rows &&
+                     pc_desc_bytes(n_rows, n_segments) <= resident_desc_bytes(n_rows);
+  // (default: the 1-term levels; RQSID_PC=2 takes the 3-term ones too, RQSID_PC=0 none)
+  const int pc_mode = pce ? atoi(pce) : 1;
+  const bool use_pc = pc_ok && (variant == 9 || (variant == 0 && (pc_mode >= 2 || (pc_mode == 1 && !t3))));
+  if (use_pc) {
+    // R-row tile offsets in the compact-list area, the tile map in the tile_seg slot, the tile descriptors in
+    // the resident screen's descriptor area; a failed launch returns before the compaction and re-score
+    int4* desc = reinterpret_cast<int4*>(work_idx + (n_rows * 4 + 255) / 256 * 64);
+    if ((rc = launch_pc_screen(p, t3, res_levels, norm, tile_seg, work_idx, desc, n_rows, st))) return rc;
+    if ((rc = check_launch("assign_pc"))) return rc;
+    hipLaunchKernelGGL(sentinel_compact_kernel, dim3((unsigned)cdiv(n_rows, kCompactRows)), dim3(256), 0, st, out_global,
+                       n_rows, p.work_count, work_idx, n_rows);
+    p.work_idx = work_idx;
+  } else if (use_rows) {
     // R-row tile offsets in the compact-list area, the tile map in the tile_seg slot; compact work list
     if ((rc = launch_rows_screen(p, res_levels, norm, tile_seg, work_idx, n_rows, st))) return rc;
   } else if (use_res) {
@@ -1637,7 +1656,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   // candidates, 1-term <= 512 (the XL preset's middle and last levels); RQSID_SCREEN_VARIANT=7 (or 2)
   // keeps the multi-pass screen for comparison
   const bool split = !legacy && variant != 7 && dim <= kSplitDim;
-  if (use_stream || use_res || use_rows) {
+  if (use_pc || use_stream || use_res || use_rows) {
   } else if (t3 && cand_count_max > 128 && split) launch_screen<4, kSplitS, true, true, 2>(p, res_levels, norm, grid, st);
   else if (t3) launch_screen2<4, 2, true>(p, res_levels, norm, grid, !legacy && cand_count_max <= 128, st);
   else if (cand_count_max <= 128) launch_screen2<4, 2, false>(p, res_levels, norm, grid, !legacy, st);

@@ -227,6 +227,18 @@ __device__ __forceinline__ void wait_chunks(int younger) {
   else wait_barrier<0>();
 }
 
+// the value of lane l ^ 32 (the other half of the wave): v_permlane32_swap, no LDS round trip (ds_bpermute)
+__device__ __forceinline__ int xor32(int x) {
+  const auto sw = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+  return (int)((threadIdx.x & 32) ? sw[0] : sw[1]);
+}
+__device__ __forceinline__ float xor32(float x) { return __int_as_float(xor32(__float_as_int(x))); }
+__device__ __forceinline__ double xor32(double x) {
+  const uint64_t u = (uint64_t)__double_as_longlong(x);
+  const uint64_t lo = (uint32_t)xor32((int)(uint32_t)u), hi = (uint32_t)xor32((int)(uint32_t)(u >> 32));
+  return __longlong_as_double((long long)((hi << 32) | lo));
+}
+
 __device__ __forceinline__ void push_work(const AssignParams& p, bool need, int lane, const WorkItem& w) {
   const unsigned long long m = __ballot(need);
   if (!m) return;
@@ -275,7 +287,7 @@ __device__ __forceinline__ bool pass_decide(const uint32_t (&pbits)[NW], int h, 
   int pc = 0;
 #pragma unroll
   for (int i = 0; i < NW; ++i) pc += __popc(pbits[i]);
-  const int pc_o = __shfl_xor(pc, 32);
+  const int pc_o = xor32(pc);
   const int ncand = pc + pc_o;
   const bool overflow = pc > kListPerHalf || pc_o > kListPerHalf || ncand == 0;
   const bool definitive = !overflow && ncand == 1;
@@ -283,7 +295,7 @@ __device__ __forceinline__ bool pass_decide(const uint32_t (&pbits)[NW], int h, 
 #pragma unroll
   for (int i = 0; i < NW; ++i) wv[i] = pbits[i];
   const int k0 = pass_take_first(wv, h);
-  k_out = max(k0, __shfl_xor(k0, 32));
+  k_out = max(k0, xor32(k0));
   w.n = overflow ? -1 : ncand;
   if (__builtin_amdgcn_ballot_w64(!definitive && !overflow)) {  // wave-uniform: some row needs a list
     int kk[kListPerHalf];
@@ -293,7 +305,7 @@ __device__ __forceinline__ bool pass_decide(const uint32_t (&pbits)[NW], int h, 
     int c8[kMaxList];
 #pragma unroll
     for (int j = 0; j < kListPerHalf; ++j) {
-      const int o = __shfl_xor(kk[j], 32);
+      const int o = xor32(kk[j]);
       c8[j] = kk[j] >= 0 ? kk[j] : INT_MAX;
       c8[kListPerHalf + j] = o >= 0 ? o : INT_MAX;
     }
@@ -486,6 +498,13 @@ void launch_tiling(const AssignParams& p, int R, int32_t* tile_seg, int32_t* seg
 bool rows_supported(int dim, int cand_count_max, bool t3, int rl, bool norm);
 int launch_rows_screen(const AssignParams& p, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles, int64_t cap,
                        hipStream_t st);
+
+// producer/consumer screen (assign_pc.hip): 512-d residual levels, 3-term <= 128 or 1-term <= 256 candidates
+// per segment; desc_mem: pc_desc_bytes(n_rows, n_segments) of workspace; seg_tiles: n_segments + 1 ints
+bool pc_supported(int dim, int cand_count_max, bool t3, int rl);
+int64_t pc_desc_bytes(int64_t n_rows, int32_t n_segments);
+int launch_pc_screen(const AssignParams& p, bool t3, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles,
+                     void* desc_mem, int64_t cap, hipStream_t st);
 
 // centre-resident screen (assign_resident.hip): 512-d rows, <= 256 candidates per segment (1 term) or
 // <= 128 (3 terms).  desc: resident_desc_bytes(n_rows) of workspace; seg_tile32: n_segments + 1 ints.

@@ -133,9 +133,20 @@ __global__ __launch_bounds__(1024) void bucket_scan_kernel(const int32_t* __rest
 
 constexpr int kScatterRowsPerBlock = 8192;
 
+// Every row_index write takes its position from a device counter (cursor[k], or the block's LDS copy of it).
+// The position is checked against the key's segment [row_off[k], row_off[k+1]) before the store: a count that
+// went wrong (a stale cursor, a key changed between the histogram and the scatter) drops the write and raises
+// bit kBucketErrScatter of the sticky error word instead of writing outside the segment or past row_index.
+constexpr int kBucketErrScatter = 1;
+__device__ __forceinline__ void bucket_put(int32_t pos, unsigned k, int64_t i, const int32_t* __restrict__ row_off,
+                                           int32_t* __restrict__ row_index, int32_t* __restrict__ err) {
+  if (pos >= row_off[k] && pos < row_off[k + 1]) row_index[pos] = (int32_t)i;
+  else atomicOr(err, kBucketErrScatter);
+}
 __global__ __launch_bounds__(256) void bucket_scatter_kernel(const int32_t* __restrict__ keys, int64_t n,
                                                              int S, int32_t* __restrict__ cursor,
-                                                             int32_t* __restrict__ row_index) {
+                                                             const int32_t* __restrict__ row_off,
+                                                             int32_t* __restrict__ row_index, int32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) int32_t lh[];
   if (S <= kBucketLdsBins) {
     const int64_t r0 = (int64_t)blockIdx.x * kScatterRowsPerBlock;
@@ -155,16 +166,14 @@ __global__ __launch_bounds__(256) void bucket_scatter_kernel(const int32_t* __re
     for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
       const unsigned k = (unsigned)keys[i];
       if (k >= (unsigned)S) continue;
-      const int32_t pos = atomicAdd(&lh[k], 1);
-      row_index[pos] = (int32_t)i;
+      bucket_put(atomicAdd(&lh[k], 1), k, i, row_off, row_index, err);
     }
   } else {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
       const unsigned k = (unsigned)keys[i];
       if (k >= (unsigned)S) continue;
-      const int32_t pos = atomicAdd(&cursor[k], 1);
-      row_index[pos] = (int32_t)i;
+      bucket_put(atomicAdd(&cursor[k], 1), k, i, row_off, row_index, err);
     }
   }
 }
@@ -571,10 +580,38 @@ using namespace rqsid;
 extern "C" {
 
 int rqsid_version(void) { return 1; }
+
+// Timing-probe macros this library was built with (tools/ab_build.sh; such builds return WRONG IDs by design):
+// 1 RQSID_AB_MODE, 2 RQSID_AB_HALFROW, 4 RQSID_AB_NOROWDMA, 8 RQSID_AB_EPI, 16 RQSID_STAMPS, 32 RQSID_AB_NO_FLUSH.
+// 0 for a product build; the Python loader refuses anything else unless the library was named by RQSID_LIB.
+int32_t rqsid_build_flags(void) {
+  int32_t f = 0;
+#if defined(RQSID_AB_MODE) && RQSID_AB_MODE
+  f |= 1;
+#endif
+#ifdef RQSID_AB_HALFROW
+  f |= 2;
+#endif
+#ifdef RQSID_AB_NOROWDMA
+  f |= 4;
+#endif
+#ifdef RQSID_AB_EPI
+  f |= 8;
+#endif
+#ifdef RQSID_STAMPS
+  f |= 16;
+#endif
+#ifdef RQSID_AB_NO_FLUSH
+  f |= 32;
+#endif
+  return f;
+}
 const char* rqsid_last_error(void) { return g_err; }
 
 int32_t rqsid_centroid_tile_rows(void) { return kAccTileRows; }
 
+// workspace: counts i32[S] | cursor i32[S] | 64 ints: [0] the sticky error word (zeroed by the caller when it
+// allocates the workspace, never by a call: include/rqsid.h)
 int64_t rqsid_bucket_workspace_bytes(int64_t n, int32_t n_segments) {
   (void)n;
   return ((int64_t)n_segments * 2 + 64) * 4;
@@ -605,7 +642,8 @@ int rqsid_bucket(const int32_t* keys, int64_t n, int32_t S, int32_t tile_rows, i
   if (n > 0) {
     const unsigned blocks = S <= kBucketLdsBins ? (unsigned)cdiv(n, kScatterRowsPerBlock)
                                                 : grid_cap(cdiv(n, 256 * 16), 2048);
-    hipLaunchKernelGGL(bucket_scatter_kernel, dim3(blocks), dim3(256), lds, st, keys, n, S, cursor, row_index);
+    hipLaunchKernelGGL(bucket_scatter_kernel, dim3(blocks), dim3(256), lds, st, keys, n, S, cursor, seg_row_off,
+                       row_index, cursor + S);
     if ((rc = check_launch("bucket_scatter"))) return rc;
   }
   return RQSID_OK;

@@ -385,10 +385,36 @@ class ShardedAuction:
         dist.all_gather(parts, src, group=self.group)
         return [p.to(t.device) for p in parts]
 
+    # environment switches librqsid reads on each rank for the row-sharded list rounds (auction_seg.hip
+    # seg_carve / rqsid_dauction_begin): they decide lkb, the list start and whether lists run at all, so
+    # ranks that disagree would split between list and sweep slots inside the same collectives
+    _SETTINGS = ("RQSID_DAUCTION_LIST", "RQSID_LIST_DELTA", "RQSID_LIST_START")
+
+    def _check_uniform_settings(self) -> None:
+        """Raise unless every rank of the group runs with the same list settings (two tiny all_reduces)."""
+        import os
+        vals = []
+        for name in self._SETTINGS:
+            v = os.environ.get(name)
+            try:
+                vals.append(-1 if v is None else int(v))
+            except ValueError:
+                vals.append(-2)
+        dev = torch.device("cpu") if self.stage else torch.device("cuda", torch.cuda.current_device())
+        lo = torch.tensor(vals, dtype=torch.int64, device=dev)
+        hi = lo.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+        if not torch.equal(lo, hi):
+            raise RuntimeError(f"sharded auction: ranks disagree on {dict(zip(self._SETTINGS, vals))} "
+                               f"(min {lo.tolist()}, max {hi.tolist()}); set them alike on every rank")
+
     def run(self, passes, n_global: int, k: int, max_rounds: int = 0):
         """Returns (this rank's assignment, rounds run)."""
         if n_global == 0:
             return passes.result(), 0
+        if self.world > 1:
+            self._check_uniform_settings()
         if k == 1:
             raise ValueError("auction: a single worker cannot bid on N + 1 jobs")
         mm = passes.begin()
@@ -419,7 +445,9 @@ class ShardedAuction:
                 continue
             if not passes.live():
                 return passes.result(), passes.rounds_run()
-            if max_rounds and issued >= max_rounds:
+            # the cap counts real rounds: a void list slot (rounds from lists that did not hold) advances no
+            # round, so the number of slots issued may exceed the rounds run
+            if max_rounds and passes.rounds_run() >= max_rounds:
                 raise RuntimeError(f"auction: no complete assignment after {max_rounds} rounds")
             if _STATS and hasattr(passes, "debug"):
                 print("dauction slot", issued, passes.debug(), flush=True)

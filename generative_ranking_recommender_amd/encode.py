@@ -86,13 +86,31 @@ class RQEncoder:
             # bitwise-duplicate centres can never be the first minimum: drop them from the lists
             self.cands.append(ops.dedup_candidates(c, self.pcs[l].centers))
         self._ws = None
+        self._bws = {}  # n_segments -> reusable rqsid_bucket workspace (sticky error word)
         self.last_rescored = []
         self.force_materialized = False
 
     def _workspace(self, n):
         if self._ws is None or self._ws.n_rows < n:
+            if self._ws is not None:  # a bigger workspace replaces it: keep what its word recorded
+                ops.check_error_words([self._ws.error_word()], "RQEncoder")
             self._ws = ops.AssignWorkspace(n, self.device)
         return self._ws
+
+    def _bucket(self, keys, n_segments):
+        ws = self._bws.get(n_segments)
+        if ws is None:
+            ws = self._bws[n_segments] = ops.bucket_workspace(n_segments, self.device)
+        return ops.bucket(keys, n_segments, workspace=ws)
+
+    def error_words(self):
+        """Device views of the sticky error words this encoder's calls write (assign and bucketing)."""
+        return ([self._ws.error_word()] if self._ws is not None else []) + \
+            [ops.bucket_error_word(w, s) for s, w in self._bws.items()]
+
+    def check_errors(self) -> None:
+        """Raise RuntimeError if any counter-driven write of this encoder's calls was dropped (one host sync)."""
+        ops.check_error_words(self.error_words(), "RQEncoder.encode")
 
     def _weighted(self, x, l):
         if self.weights is None:
@@ -116,9 +134,13 @@ class RQEncoder:
             return False
         return True
 
-    def encode(self, x: torch.Tensor, count_rescored: bool = False) -> torch.Tensor:
+    def encode(self, x: torch.Tensor, count_rescored: bool = False, check: Optional[bool] = None) -> torch.Tensor:
         """x: f32 [N, D] on the device -> int32 [N, L] semantic IDs (a transposed view of the
-        level-major [L, N] buffer the kernels write; no copy)."""
+        level-major [L, N] buffer the kernels write; no copy).  ``check`` (default: on unless the stream is
+        being captured into a graph): read the device error words after the call (one host sync) and raise
+        if a counter-driven list write was dropped; a captured step checks with ``check_errors()``."""
+        if check is None:
+            check = not torch.cuda.is_current_stream_capturing()
         if x.dim() != 2 or x.shape[1] != self.dim:
             raise ValueError(f"Input dimension {x.shape[-1]} does not match config embedding_dim {self.dim}")
         x = x.float().contiguous()
@@ -135,6 +157,8 @@ class RQEncoder:
             self._encode_fused(x, out, ws, count_rescored)
         else:
             self._encode_materialized(x, out, ws, count_rescored)
+        if check:
+            self.check_errors()
         return out.t()
 
     def _last_level_buckets(self, out, l, n, device):
@@ -149,7 +173,7 @@ class RQEncoder:
                 gmax = int(grp.max().item())
                 if gmax >= self.n_groups:
                     raise IndexError(f"index {gmax} is out of bounds for axis 0 with size {self.n_groups}")
-            return ops.bucket(grp, self.n_groups)
+            return self._bucket(grp, self.n_groups)
         return ops.single_segment(n, device)
 
     def _finish_last(self, out, l, glob):
@@ -174,7 +198,7 @@ class RQEncoder:
             return
         n1 = torch.empty(n, dtype=torch.float32, device=dev) if norm else None
         glob1 = torch.empty(n, dtype=torch.int32, device=dev)
-        b = ops.bucket(out[0], self.need[0]) if self.L == 3 else self._last_level_buckets(out, 1, n, dev)
+        b = self._bucket(out[0], self.need[0]) if self.L == 3 else self._last_level_buckets(out, 1, n, dev)
         fr1 = ops.FusedResidual(1, norm, self.pcs[0].centers, None, den_out=n1)
         ops.assign(x, self.pcs[1], b, self.cands[1], out_local=out[1], out_global=glob1, workspace=ws, fused=fr1)
         if count_rescored:
@@ -213,7 +237,7 @@ class RQEncoder:
                 ops.assign(w, self.pcs[0], b, self.cands[0], out_local=out[0], out_global=glob, workspace=ws)
                 out[0].copy_(glob)
             elif l < self.L - 1:
-                b = ops.bucket(out[l - 1], self.need[l - 1])
+                b = self._bucket(out[l - 1], self.need[l - 1])
                 ops.assign(w, self.pcs[l], b, self.cands[l], out_local=out[l], out_global=glob, workspace=ws)
             else:
                 b = self._last_level_buckets(out, l, n, x.device)

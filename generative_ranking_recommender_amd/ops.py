@@ -93,6 +93,23 @@ class Buckets:
     row_index: Optional[torch.Tensor]  # i32 [N] or None (identity)
     n_segments: int
     max_tiles: int
+    workspace: Optional[torch.Tensor] = None  # rqsid_bucket's workspace (its sticky error word: error_word())
+
+    def error_word(self) -> Optional[torch.Tensor]:
+        """Device view of the workspace's sticky error word (include/rqsid.h rqsid_bucket), or None."""
+        return None if self.workspace is None else bucket_error_word(self.workspace, self.n_segments)
+
+
+def bucket_workspace(n_segments: int, device) -> torch.Tensor:
+    """A reusable rqsid_bucket workspace with its sticky error word zeroed (the caller's duty)."""
+    wsb = int(lib().rqsid_bucket_workspace_bytes(0, n_segments))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=device)
+    bucket_error_word(ws, n_segments).zero_()
+    return ws
+
+
+def bucket_error_word(ws: torch.Tensor, n_segments: int) -> torch.Tensor:
+    return ws[8 * n_segments:8 * n_segments + 4].view(torch.int32)
 
 
 def single_segment(n: int, device, rows_per_tile: Optional[int] = None) -> Buckets:
@@ -104,7 +121,10 @@ def single_segment(n: int, device, rows_per_tile: Optional[int] = None) -> Bucke
     return Buckets(off, toff, None, 1, (n + tr - 1) // tr)
 
 
-def bucket(keys: torch.Tensor, n_segments: int, rows_per_tile: Optional[int] = None) -> Buckets:
+def bucket(keys: torch.Tensor, n_segments: int, rows_per_tile: Optional[int] = None,
+           workspace: Optional[torch.Tensor] = None) -> Buckets:
+    """Counting sort of rows by key.  ``workspace``: a reusable ``bucket_workspace(n_segments)`` whose sticky
+    error word accumulates over calls (default: a fresh one per call)."""
     keys = keys.to(torch.int32).contiguous()
     _require_device(keys)
     n = keys.numel()
@@ -113,10 +133,10 @@ def bucket(keys: torch.Tensor, n_segments: int, rows_per_tile: Optional[int] = N
     toff = torch.empty(n_segments + 1, dtype=torch.int32, device=keys.device)
     idx = torch.empty(max(n, 1), dtype=torch.int32, device=keys.device)
     wsb = int(lib().rqsid_bucket_workspace_bytes(n, n_segments))
-    ws = torch.empty(wsb, dtype=torch.uint8, device=keys.device)
+    ws = workspace if workspace is not None and workspace.numel() >= wsb else bucket_workspace(n_segments, keys.device)
     _lib.check(lib().rqsid_bucket(_ptr(keys), n, n_segments, tr, _ptr(off), _ptr(toff), _ptr(idx), _ptr(ws), wsb,
                                   _stream()), "rqsid_bucket")
-    return Buckets(off, toff, idx[:n], n_segments, (n + tr - 1) // tr + n_segments)
+    return Buckets(off, toff, idx[:n], n_segments, (n + tr - 1) // tr + n_segments, ws)
 
 
 @dataclass
@@ -205,7 +225,22 @@ class AssignWorkspace:
         """Sticky error word of every assign on this workspace (host sync; csrc/assign.hip kErrSlot):
         bit 0 compaction past n_rows, bit 1 overflow list past n_rows, bit 2 a list entry outside work[].
         Every such write is bounded by its slot's capacity; a non-zero word means one was dropped."""
-        return int(self.buf[240:244].view(torch.int32).item())
+        return int(self.error_word().item())
+
+    def error_word(self) -> torch.Tensor:
+        return self.buf[240:244].view(torch.int32)
+
+
+def check_error_words(words, what: str) -> None:
+    """One host sync over device error words (AssignWorkspace / Buckets); raise if any is non-zero: a
+    counter-driven write was dropped, so the IDs of that call are not trustworthy."""
+    ws = [w for w in words if w is not None]
+    if not ws:
+        return
+    vals = torch.cat(ws).cpu().tolist()
+    if any(vals):
+        raise RuntimeError(f"{what}: a device error word is set ({vals}): a counter-driven list write fell outside "
+                           "its slot and was dropped (csrc/assign.hip kErrSlot, rqsid_bucket)")
 
 
 @dataclass

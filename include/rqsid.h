@@ -37,6 +37,10 @@ extern "C" {
 
 int rqsid_version(void);
 const char* rqsid_last_error(void);
+/* 0 for a product build; else the bits of the timing-probe macros it was compiled with (tools/ab_build.sh:
+ * 1 RQSID_AB_MODE, 2 RQSID_AB_HALFROW, 4 RQSID_AB_NOROWDMA, 8 RQSID_AB_EPI, 16 RQSID_STAMPS,
+ * 32 RQSID_AB_NO_FLUSH) -- such a library returns wrong IDs by design and must never ship. */
+int32_t rqsid_build_flags(void);
 
 /* Centre preparation for rqsid_assign.  The table is scaled by a power of two 2^s (largest element
  * just below 2^14) and split into two fp16 terms: hi = fp16(c 2^s) and lo = fp16((c 2^s - hi) 2^12),
@@ -61,7 +65,11 @@ int rqsid_prepare_centers_hi(const uint16_t* c16, int64_t k, int32_t dim, uint16
  * ceil(rows_in_segment / tile_rows)), row_index[n] (rows grouped by key).
  * Replaces the per-parent torch.where/mask loops of
  * hierarchical_rq_kmeans.py:711,880-885,1210-1216 and
- * simplified_semantic_id_generator.py:112,154-158,263. */
+ * simplified_semantic_id_generator.py:112,154-158,263.
+ * Workspace int 2*n_segments (the first int after counts and cursors) is a sticky error word the
+ * caller zeroes when it allocates the workspace (a call never clears it): every row_index write takes
+ * its position from a device counter, and a position outside its key's segment drops the write and
+ * sets bit 1 there (a wrong count can only report an error, never store outside row_index). */
 int64_t rqsid_bucket_workspace_bytes(int64_t n, int32_t n_segments);
 int rqsid_bucket(const int32_t* keys, int64_t n, int32_t n_segments, int32_t tile_rows,
                  int32_t* seg_row_off, int32_t* seg_tile_off, int32_t* row_index,

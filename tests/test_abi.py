@@ -51,3 +51,38 @@ def test_argument_errors_map_to_value_error():
     assert "prepare_centers" in lib.rqsid_last_error().decode()
     with pytest.raises(ValueError):
         _lib.check(rc, "rqsid_prepare_centers")
+
+
+def test_product_build_has_no_probe_flags():
+    """a timing-probe build (RQSID_AB_*, RQSID_STAMPS) returns wrong IDs by design; the in-tree
+    library must report none, and the loader refuses one unless RQSID_LIB names it explicitly."""
+    assert _lib.load().rqsid_build_flags() == 0
+
+
+def test_pc_kernel_keeps_nothing_in_m0():
+    """assign_pc.hip drops the M0 save/restore around its LDS-DMA asm (RQ_M0_KEEP 0): valid only while hipcc
+    itself neither reads nor writes M0 anywhere in assign_pc_kernel outside those asm blocks."""
+    import shutil
+    import tempfile
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not Path(hipcc).exists():
+        pytest.skip("hipcc not available")
+    src = REPO / "generative_ranking_recommender_amd" / "csrc" / "assign_pc.hip"
+    with tempfile.TemporaryDirectory() as d:
+        asm = Path(d) / "pc.s"
+        subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "--cuda-device-only",
+                        "-S", "-o", str(asm), str(src)], check=True, capture_output=True)
+        text = asm.read_text()
+    kernels = re.findall(r"^(_Z\w*assign_pc_kernel\w*):", text, re.M)
+    assert kernels
+    for k in kernels:
+        body = text[text.index(k + ":"):text.index(".Lfunc_end", text.index(k + ":"))]
+        inside, bad = False, []
+        for line in body.splitlines():
+            if "ASMSTART" in line:
+                inside = True
+            elif "ASMEND" in line:
+                inside = False
+            elif not inside and re.search(r"\bm0\b", line.split(";")[0]):
+                bad.append(line.strip())
+        assert not bad, (k, bad[:5])

@@ -617,3 +617,39 @@ def test_regroup_rows_orders_like_one_process(world):
     for r, (_, xs, kk, lst) in enumerate(res):
         assert ((kk >= bounds[r]) & (kk < bounds[r + 1])).all()
         assert [len(t) for t in lst] == list(range(1, world + 1))
+
+
+def _settings_worker(rank, world, port, out):
+    from generative_ranking_recommender_amd.distributed import ShardedAuction
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if rank == 1:
+        os.environ["RQSID_LIST_DELTA"] = "16"  # librqsid reads it per rank (auction_seg.hip): ranks disagree
+    else:
+        os.environ.pop("RQSID_LIST_DELTA", None)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n, k = 64, 8
+    rng = np.random.default_rng(5)
+    w16 = (-rng.integers(1, 4, size=(k, n)).astype(F32)).astype(np.float16)
+    s, e = shard_bounds(n, rank, world)
+    try:
+        ShardedAuction().run(NumpyAuctionPasses(w16[:, s:e], n), n, k, max_rounds=3000)
+        out.put((rank, "ran"))
+    except RuntimeError as ex:
+        out.put((rank, str(ex)))
+    dist.destroy_process_group()
+
+
+def test_sharded_auction_refuses_ranks_with_different_list_settings():
+    """the row-sharded list rounds read RQSID_DAUCTION_LIST / RQSID_LIST_DELTA / RQSID_LIST_START on
+    each rank; ranks that disagree would split between list and sweep slots inside the same collectives.
+    ShardedAuction.run compares them over the group first (MIN == MAX) and every rank raises."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_settings_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(60)
+    assert all("ranks disagree" in v for v in res.values()), res

@@ -6,6 +6,6 @@ cd "$(dirname "$0")/.."
 C=generative_ranking_recommender_amd/csrc
 for m in ${MODES:-1 2 3}; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize -shared -fPIC -DRQSID_AB_MODE=$m ${EXTRA:-} \
-    -o tools/ab/librqsid_ab$m${SUFFIX:-}.so $C/rqsid.hip $C/assign.hip $C/assign_stream.hip $C/assign_resident.hip $C/assign_rows.hip $C/auction.hip $C/auction_seg.hip &
+    -o tools/ab/librqsid_ab$m${SUFFIX:-}.so $C/rqsid.hip $C/assign.hip $C/assign_stream.hip $C/assign_resident.hip $C/assign_rows.hip $C/assign_pc.hip $C/auction.hip $C/auction_seg.hip &
 done
 for j in $(jobs -p); do wait $j || { echo "ab_build failed"; exit 1; }; done
