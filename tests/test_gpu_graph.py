@@ -52,10 +52,11 @@ def test_encode_step_graph_replays_equal_eager():
 
 
 def test_encode_list_writes_stay_in_bounds():
-    """Every list write of rqsid_assign whose index comes from a device counter (the sentinel compaction
-    of the streamed screens, the overflow list of the fp32 re-screen) is bounded by its slot and raises a
-    bit of the workspace's sticky error word instead of writing past it (csrc/assign.hip kErrSlot).  PROD
-    codebooks, every level, eager and three back-to-back graph replays: the word stays 0."""
+    """Every write of the captured encode step whose index comes from a device counter -- rqsid_assign's
+    sentinel compaction and the fp32 re-screen's overflow list (csrc/assign.hip kErrSlot), rqsid_bucket's
+    row_index scatter (csrc/rqsid.hip bucket_put) -- is bounded by its slot and raises a bit of a sticky error
+    word instead of writing past it.  PROD codebooks, every level, eager and three back-to-back graph
+    replays: every word stays 0 (the encoder's assign workspace and both of its bucket workspaces)."""
     dev = torch.device("cuda", 0)
     cb = synth.encode_codebooks(seed=99)
     enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], [128, 128, 256],
@@ -77,4 +78,20 @@ def test_encode_list_writes_stay_in_bounds():
     torch.cuda.synchronize()
     assert torch.equal(out, eager)
     assert enc._ws.error() == 0
+    words = enc.error_words()
+    assert len(words) == 3 and all(int(w.item()) == 0 for w in words)  # assign + the two levels' buckets
     del g
+
+
+def test_encode_raises_on_a_set_error_word():
+    """a dropped counter-driven write must not pass silently.  RQEncoder.encode reads the error
+    words after the call (one host sync) and raises; here a bucket word is set by hand."""
+    dev = torch.device("cuda", 0)
+    cb = synth.encode_codebooks(seed=5, need=(16, 16, 32), n_cand=320, pool_rows=8192)
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], [16, 16, 32],
+                    match=torch.from_numpy(cb["match"]), semantics=HIERARCHICAL_TRAIN, device=dev)
+    x = torch.from_numpy(synth.mixture_rows(0, 4096)).to(dev)
+    enc.encode(x)
+    enc.error_words()[-1].fill_(1)
+    with pytest.raises(RuntimeError, match="error word"):
+        enc.encode(x)
