@@ -11,7 +11,7 @@ ARGS="--steps 2 --warmup 1 --no-cpu --balanced-rows 0 --train-iters 0 --parity-r
 i=0
 for c in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
-  (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "assign_screen|assign_stream|assign_pp|assign_resident|assign_rows|assign_rescreen|assign_rescore" \
+  (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "assign_screen|assign_stream|assign_pp|assign_pc|assign_resident|assign_rows|assign_rescreen|assign_rescore" \
      --output-format csv -d "$OUT/p$i" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" $ARGS > "$OUT/p$i.log" 2>&1)
   rc=$?; echo "pass $c rc=$rc"
   [ $rc -ne 0 ] && { tail -5 "$OUT/p$i.log"; exit $rc; }
