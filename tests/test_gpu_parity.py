@@ -423,7 +423,10 @@ STREAMED = {"default": {"RQSID_SCREEN_VARIANT": 0},
             # the row-resident screen (assign_rows.hip) wherever it applies (1-term levels: L0 and L2 here)
             "rows443": {"RQSID_SCREEN_VARIANT": 8, "RQSID_ROWS_SHAPE": 443},
             "rows482": {"RQSID_SCREEN_VARIANT": 8, "RQSID_ROWS_SHAPE": 482},
-            "rows883": {"RQSID_SCREEN_VARIANT": 8, "RQSID_ROWS_SHAPE": 883}}
+            "rows883": {"RQSID_SCREEN_VARIANT": 8, "RQSID_ROWS_SHAPE": 883},
+            # the producer/consumer screen (assign_pc.hip) on levels 1 and 2: wide (256-row) and 128-row forms
+            "pc128": {"RQSID_SCREEN_VARIANT": 9},
+            "pcw": {"RQSID_SCREEN_VARIANT": 9, "RQSID_PCW": 1}}
 
 
 @pytest.mark.parametrize("form", list(STREAMED))

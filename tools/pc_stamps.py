@@ -2,7 +2,9 @@
 """Diagnostics (GPU, stamps build: EXTRA=-DRQSID_STAMPS MODES=0 SUFFIX=_st tools/ab_build.sh, loaded through
 RQSID_LIB): per encode level, the producer/consumer screen's (assign_pc.hip) cycles per wave and role --
 consumer {barrier, compute, epilogue}, row producer {DMA issue, vmcnt wait, build, finish, barrier},
-loader {DMA issue, vmcnt wait, barrier} -- as shares of the role's total and as cycles per chunk phase."""
+loader {DMA issue, vmcnt wait, barrier} -- as shares of the role's total and as cycles per chunk phase.
+The wide form (assign_pcw_kernel, 256-row tiles, RQSID_PCW unset or 1): consumer {barrier, compute,
+epilogue}, feeder {DMA issue, build, vmcnt wait, barrier}; PCW=1 in the environment selects that table."""
 import ctypes
 import os
 import sys
@@ -49,18 +51,23 @@ def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000))):
     encmod.ops.assign = hook
     enc.encode(x)
     encmod.ops.assign = orig
+    wide = os.environ.get("PCW", "0") == "1"
+    rows_t, ph_t, ncons = (256, 32, 8) if wide else (128, 16, 4)
     names = {0: ("consumer", {1: "barrier", 5: "compute", 3: "epilogue"}),
              8: ("producer", {6: "issue", 2: "vmcnt", 5: "build", 3: "finish", 1: "barrier"}),
              16: ("loader", {6: "issue", 2: "vmcnt", 1: "barrier"})}
+    if wide:
+        names = {0: ("consumer", {1: "barrier", 5: "compute", 3: "epilogue"}),
+                 8: ("feeder", {6: "issue", 5: "build", 2: "vmcnt", 1: "barrier"})}
     for lvl, (b, v) in enumerate(res):
         waves = v[4]
         if not waves:
             print(f"L{lvl}: producer/consumer screen not used")
             continue
         rows = int(b.seg_row_off[-1].item())
-        tiles = int(((b.seg_row_off[1:] - b.seg_row_off[:-1] + 127) // 128).sum().item())
-        phases = 16.0 * tiles / (waves / 4)  # chunk phases per block (4 consumer waves per block)
-        line = [f"L{lvl}: rows={rows} tiles={tiles} blocks={waves // 4} phases/block={phases:.0f}"]
+        tiles = int(((b.seg_row_off[1:] - b.seg_row_off[:-1] + rows_t - 1) // rows_t).sum().item())
+        phases = ph_t * tiles / (waves / ncons)  # phases per block
+        line = [f"L{lvl}: rows={rows} tiles={tiles} blocks={waves // ncons} phases/block={phases:.0f}"]
         for base, (role, parts) in names.items():
             w = v[base + 4]
             tot = v[base] / w
