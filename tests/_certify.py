@@ -102,18 +102,33 @@ def certify_step(x: np.ndarray, c_in: np.ndarray, scores_wk16, assign, c_out: np
     return diverged
 
 
+COUNTERS = ("steps", "auctions", "tie_divergences", "order_flips", "scores", "divergent_steps", "loss_divergences")
+
+
 def new_stats():
-    return {"steps": 0, "auctions": 0, "tie_divergences": 0, "order_flips": 0, "scores": 0, "divergent_steps": 0,
-            "loss_divergences": 0, "segments": {}}
+    return {**{k: 0 for k in COUNTERS}, "segments": {}}
 
 
-def _mark(stats, key, window, diverged):
+def _mark(stats, key, window, diverged, delta):
+    """record one certified step of segment ``key`` in lockstep window ``window``: a later window replaces
+    the segment's record (fit_segments re-ran it; the earlier attempt's result was discarded)"""
     cur = stats["segments"].get(key)
     if cur is None or window > cur["window"]:
-        cur = stats["segments"][key] = {"window": window, "diverged": False, "steps": 0}
+        cur = stats["segments"][key] = {"window": window, "diverged": False, **{k: 0 for k in COUNTERS}}
     if window == cur["window"]:
         cur["diverged"] |= bool(diverged)
-        cur["steps"] += 1
+        for k in COUNTERS:
+            cur[k] += delta[k]
+
+
+def summary(stats) -> dict:
+    """the counters split by what the run kept: ``kept`` sums the attempts whose results the fit returned
+    (the steps the exactness claims rest on); ``discarded`` the speculative lockstep windows fit_segments
+    threw away and re-ran; ``all`` both (every traced, certified step)"""
+    kept = {k: sum(v[k] for v in stats["segments"].values()) for k in COUNTERS}
+    total = {k: stats[k] for k in COUNTERS}
+    return {"all": total, "kept": kept, "discarded": {k: total[k] - kept[k] for k in COUNTERS},
+            "kept_divergent_segments": sum(bool(v["diverged"]) for v in stats["segments"].values())}
 
 
 def certify_trace(events, stats=None):
@@ -130,8 +145,9 @@ def certify_trace(events, stats=None):
         x, half = xs[key], bool(ev["half"])
         c_in, c_out = _np(ev["centers_in"]), _np(ev["centers_out"])
         if ev["kind"] == "fit":
+            before = {k: stats[k] for k in COUNTERS}
             dv = certify_step(x, c_in, ev["scores"], ev["assign"], c_out, half, stats, ev.get("loss"), ev.get("target"))
-            _mark(stats, (ev["owner"], 0), 0, dv)
+            _mark(stats, (ev["owner"], 0), 0, dv, {k: stats[k] - before[k] for k in COUNTERS})
             continue
         off, act = ev["off"], ev["active"]
         k = len(c_in) // (len(off) - 1)
@@ -141,9 +157,11 @@ def certify_trace(events, stats=None):
         for s in np.nonzero(act)[0]:
             r0, r1 = int(off[s]), int(off[s + 1])
             blk = None if w is None else w[k * r0:k * r1]
+            before = {k: stats[k] for k in COUNTERS}
             dv = certify_step(x[r0:r1], c_in[s * k:(s + 1) * k], blk, a[r0:r1], c_out[s * k:(s + 1) * k], half, stats,
                               None if loss is None else loss[s], ev.get("target"))
-            _mark(stats, (ev["owner"], ev["seg_base"] + int(s)), ev["window"], dv)
+            _mark(stats, (ev["owner"], ev["seg_base"] + int(s)), ev["window"], dv,
+                  {kk: stats[kk] - before[kk] for kk in COUNTERS})
     return stats
 
 

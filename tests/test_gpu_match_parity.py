@@ -121,7 +121,7 @@ def test_hierarchical_match_matrix_matches_reference(golden, tracer):
     diverged = _certify.diverged_segments(st, owners[0])
     identical, excused, sync = _compare_builder(g, "hier", np.asarray(got), fitted, diverged, np_after, torch_after)
     report("hier_match_matrix", identical_rows=identical, excused=excused, rng_in_sync=sync, fitted=len(fitted),
-           diverged_fits=sorted(diverged), **{k: v for k, v in st.items() if k != "segments"})
+           diverged_fits=sorted(diverged), **_certify.summary(st))
 
 
 def test_simplified_match_matrix_matches_reference(golden, tracer):
@@ -140,7 +140,7 @@ def test_simplified_match_matrix_matches_reference(golden, tracer):
     identical, excused, sync = _compare_builder(g, "simp", got.numpy().astype(np.uint8), fitted, diverged, np_after,
                                                 torch_after)
     report("simp_match_matrix", identical_rows=identical, excused=excused, rng_in_sync=sync, fitted=len(fitted),
-           diverged_fits=sorted(diverged), **{k: v for k, v in st.items() if k != "segments"})
+           diverged_fits=sorted(diverged), **_certify.summary(st))
 
 
 def test_match_builders_sequential_and_lockstep_agree_on_golden_inputs(golden):

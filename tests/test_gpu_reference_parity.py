@@ -142,7 +142,7 @@ def test_balanced_fit_certified_against_reference(golden, tracer):
     sse_ref, sse_got = _certify.sse(x, g["fit_bal_centers"], g["fit_bal_assign"]), _certify.sse(x, c, a)
     assert sse_got <= sse_ref * (1 + SSE_RTOL)
     report("fit_balanced", identical=same, agree=float((a == g["fit_bal_assign"]).mean()), sse_ref=sse_ref,
-           sse_gpu=sse_got, **{k: v for k, v in st.items() if k != "segments"})
+           sse_gpu=sse_got, **_certify.summary(st))
 
 
 def test_fit_by_min_loss_certified_against_reference(golden, tracer):
@@ -167,7 +167,7 @@ def test_fit_by_min_loss_certified_against_reference(golden, tracer):
     sse_ref, sse_got = _certify.sse(x, ref, a_ref), _certify.sse(x, c, a_got)
     assert sse_got <= sse_ref * (1 + SSE_RTOL)
     report("fit_by_min_loss", identical=close, max_center_diff=float(np.abs(c - ref).max()), sse_ref=sse_ref,
-           sse_gpu=sse_got, **{k: v for k, v in st.items() if k != "segments"})
+           sse_gpu=sse_got, **_certify.summary(st))
 
 
 # ------------------------------------------------------------------------------- trainers (A12, A13)
@@ -237,7 +237,7 @@ def test_hierarchical_train_certified_against_reference(golden, tracer):
     uniq_ref, uniq_got = len(np.unique(ref, axis=0)), len(np.unique(ids, axis=0))
     assert uniq_got >= 0.9 * uniq_ref
     report("hierarchical_train", agree_per_level=(ids == ref).mean(0), sse_ref=sse_ref, sse_gpu=sse_got,
-           exact=exact, unique_ref=uniq_ref, unique_gpu=uniq_got, **{k: v for k, v in st.items() if k != "segments"})
+           exact=exact, unique_ref=uniq_ref, unique_gpu=uniq_got, **_certify.summary(st))
 
 
 def test_simplified_train_certified_against_reference(golden, tracer, tmp_path):
@@ -270,7 +270,7 @@ def test_simplified_train_certified_against_reference(golden, tracer, tmp_path):
     assert c_got.max() - c_got.min() <= max(2, c_ref.max() - c_ref.min() + 2)
     report("simplified_train", agree_per_level=(ids == ref).mean(0), sse_ref=sse_ref, sse_gpu=sse_got, exact=exact,
            unique_ref=len(np.unique(ref, axis=0)), unique_gpu=len(np.unique(ids, axis=0)),
-           **{k: v for k, v in st.items() if k != "segments"})
+           **_certify.summary(st))
 
 
 # ------------------------------------------------------------- exact-branch fixtures
@@ -301,7 +301,7 @@ def test_hierarchical_train_exact_against_reference(golden, tracer):
     exact = _cascade(st, tracer.events, ids, g["hier_ids"], cents, ref_cents, need, match, g["hier_match"])
     report("hierarchical_train_exact", exact=exact, agree_per_level=(ids == g["hier_ids"]).mean(0),
            max_center_diff=[float(np.abs(a - b).max()) for a, b in zip(cents, ref_cents)],
-           **{k: v for k, v in st.items() if k != "segments"})
+           **_certify.summary(st))
     assert _no_step_diverged(st)
     assert exact == {"level0": True, "parents": need[0], "candidates": True, "groups": True}, exact
     assert np.array_equal(ids, g["hier_ids"])
@@ -335,7 +335,7 @@ def test_simplified_train_exact_against_reference(golden, tracer, tmp_path):
     same_bytes = synth.sha256(np.frombuffer(out.read_bytes(), dtype=np.uint8)) == str(g["simp_jsonl_sha"])
     report("simplified_train_exact", exact=exact, agree_per_level=(ids == g["simp_ids"]).mean(0), jsonl=same_bytes,
            max_center_diff=[float(np.abs(a - b).max()) for a, b in zip(cents, ref_cents)],
-           **{k: v for k, v in st.items() if k != "segments"})
+           **_certify.summary(st))
     assert _no_step_diverged(st)
     assert exact == {"level0": True, "parents": need[0], "candidates": True, "groups": True}, exact
     assert np.array_equal(ids, g["simp_ids"])
@@ -385,7 +385,7 @@ def test_candidate_fit_half_k1280_certified(tracer):
     st = _certify.certify_trace(tracer.events)
     assert st["steps"] == 2 and st["auctions"] == 2
     assert np.bincount(a, minlength=1280).max() == 2
-    report("candidate_fit_k1280_half", **{k: v for k, v in st.items() if k != "segments"})
+    report("candidate_fit_k1280_half", **_certify.summary(st))
 
 
 @pytest.mark.parametrize("tag", sorted(_data.CONFIG0_CASES))
