@@ -918,10 +918,7 @@ constexpr int kOvfSlot = 56;  // workspace header int: overflow item count
 // caller zeroes it when it allocates the workspace; ops.AssignWorkspace.error() / RQEncoder.errors() read it).  Each index such a write takes from a device counter is
 // checked against its slot's capacity; a write that would fall outside is dropped and its bit raised, so
 // a wrong count can only produce a reported error, never a store outside the workspace.
-constexpr int kErrSlot = 60;
-constexpr int kErrCompact = 1;   // sentinel compaction: more listed rows than n_rows
-constexpr int kErrOvfList = 2;   // overflow list: more overflow items than n_rows
-constexpr int kErrWorkIdx = 4;   // a work-list entry outside [0, n_rows)
+// (kErrSlot and its bits: assign_common.h)
 template <int RL, bool NORM>
 __global__ __launch_bounds__(256) void assign_rescore_half_kernel(AssignParams p, const int32_t* __restrict__ ovf_list,
                                                                   int mode) {

@@ -345,6 +345,14 @@ __device__ __forceinline__ float wave_max(float v) {
 #define RQSID_PACKED_MAIN 0
 #endif
 
+// workspace header int 60 of rqsid_assign: the sticky error word of the counter-driven writes (assign.hip
+// kOvfSlot comment); one bit per list whose device-counted index was found past its slot
+constexpr int kErrSlot = 60;
+constexpr int kErrCompact = 1;   // sentinel compaction: more listed rows than n_rows
+constexpr int kErrOvfList = 2;   // overflow list: more overflow items than n_rows
+constexpr int kErrWorkIdx = 4;   // a work-list entry outside [0, n_rows)
+constexpr int kErrTiles = 8;     // tile count (seg_tiles[n_segments]) above the tile maps' capacity
+
 // Running sums of a row the screening bound needs (even / odd elements in .x / .y).
 struct RowSums {
   f2 se2v = {0.f, 0.f};  // sum (v - fp16(v))^2

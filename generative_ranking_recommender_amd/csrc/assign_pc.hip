@@ -128,7 +128,7 @@ __global__ __launch_bounds__(768, 3) void assign_pc_kernel(AssignParams p, const
   const uint32_t lds0 = lds_addr(smem);
 
   // XCD-contiguous tile runs (block b on XCD b % 8 walks tiles xlo + slot, + G8, ...)
-  const int ntiles = uni(seg_tiles[p.n_segments]);
+  const int ntiles = uni(seg_tiles[p.n_segments]);  // (<= max_tiles: stream_tiles_kernel clamps it)
   const int G8 = (int)(gridDim.x >> 3), xcd = (int)(blockIdx.x & 7), slot = (int)(blockIdx.x >> 3);
   const int xlo = (int)((int64_t)xcd * ntiles / 8), xhi = (int)((int64_t)(xcd + 1) * ntiles / 8);
   const int T0 = xlo + slot;
@@ -671,7 +671,7 @@ __global__ __launch_bounds__(768, 3) void assign_pcw_kernel(AssignParams p, cons
   const int h = lane >> 5, r = lane & 31;
   const uint32_t lds0 = lds_addr(smem);
 
-  const int ntiles = uni(seg_tiles[p.n_segments]);
+  const int ntiles = uni(seg_tiles[p.n_segments]);  // (<= max_tiles: stream_tiles_kernel clamps it)
   const int G8 = (int)(gridDim.x >> 3), xcd = (int)(blockIdx.x & 7), slot = (int)(blockIdx.x >> 3);
   const int xlo = (int)((int64_t)xcd * ntiles / 8), xhi = (int)((int64_t)(xcd + 1) * ntiles / 8);
   const int T0 = xlo + slot;

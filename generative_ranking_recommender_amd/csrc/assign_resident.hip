@@ -851,8 +851,10 @@ __global__ __launch_bounds__(kThreads, 1) void assign_resident_kernel(AssignPara
 #undef RS_MARK
 }
 
-// 32-row tiling of the segments: seg_tile32[s] = sum_{s' < s} ceil(rows(s') / 32) (one block)
+// 32-row tiling of the segments: seg_tile32[s] = sum_{s' < s} ceil(rows(s') / 32) (one block); the total is
+// clamped to the descriptor area's max_tiles entries, raising kErrTiles (as stream_tiles_kernel)
 __global__ __launch_bounds__(1024) void res_tiles_kernel(const int32_t* __restrict__ seg_row_off, int nseg,
+                                                         int64_t max_tiles, int32_t* __restrict__ err,
                                                          int32_t* __restrict__ seg_tile32) {
   __shared__ int part[1024];
   const int tid = threadIdx.x;
@@ -872,7 +874,14 @@ __global__ __launch_bounds__(1024) void res_tiles_kernel(const int32_t* __restri
     seg_tile32[s] = run;
     run += (seg_row_off[s + 1] - seg_row_off[s] + kRT - 1) / kRT;
   }
-  if (tid == 1023) seg_tile32[nseg] = part[1023];
+  if (tid == 1023) {
+    int total = part[1023];
+    if ((int64_t)total > max_tiles) {
+      if (err) atomicOr(err, kErrTiles);
+      total = (int)max_tiles;
+    }
+    seg_tile32[nseg] = total;
+  }
 }
 
 // tile descriptors {segment, first row position, rows} (one thread per tile)
@@ -983,7 +992,8 @@ int64_t resident_desc_bytes(int64_t n_rows) { return (n_rows > 0 ? n_rows : 0) *
 
 int launch_resident_screen(const AssignParams& p, bool t3, int rl, bool norm, int4* desc, int32_t* seg_tile32,
                            int32_t* seg_of_row, int64_t cap, hipStream_t st) {
-  hipLaunchKernelGGL(res_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, seg_tile32);
+  hipLaunchKernelGGL(res_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, cap,
+                     p.work_count ? p.work_count + kErrSlot : (int32_t*)nullptr, seg_tile32);
   hipLaunchKernelGGL(res_desc_kernel, dim3(grid_cap(cdiv(cap, 256), 4096)), dim3(256), 0, st, p.seg_row_off, seg_tile32,
                      p.n_segments, cap, desc);
   int rc = check_launch("assign_resident tiles");

@@ -1122,8 +1122,12 @@ __global__ __launch_bounds__(512, 2) void assign_pp_kernel(AssignParams p, const
 #endif
 }
 
-// 256-row tiling of the segments: seg_tile256[s] = sum_{s' < s} ceil(rows(s') / 256) (one block)
+// R-row tiling of the segments: seg_tile256[s] = sum_{s' < s} ceil(rows(s') / R) (one block).  The total,
+// which every tiled screen takes as its tile count, is clamped to the tile maps' capacity max_tiles (the
+// segment offsets of one call give at most rows / R + nseg tiles; more means a stale or doubled count): past
+// it the error word's kErrTiles bit is raised, so no screen reads a tile map or descriptor past its slot.
 __global__ __launch_bounds__(1024) void stream_tiles_kernel(const int32_t* __restrict__ seg_row_off, int nseg, int R,
+                                                            int64_t max_tiles, int32_t* __restrict__ err,
                                                             int32_t* __restrict__ seg_tile256) {
   __shared__ int part[1024];
   const int tid = threadIdx.x;
@@ -1143,7 +1147,14 @@ __global__ __launch_bounds__(1024) void stream_tiles_kernel(const int32_t* __res
     seg_tile256[s] = run;
     run += (seg_row_off[s + 1] - seg_row_off[s] + R - 1) / R;
   }
-  if (tid == 1023) seg_tile256[nseg] = part[1023];
+  if (tid == 1023) {
+    int total = part[1023];
+    if ((int64_t)total > max_tiles) {
+      if (err) atomicOr(err, kErrTiles);
+      total = (int)max_tiles;
+    }
+    seg_tile256[nseg] = total;
+  }
 }
 
 // tile -> segment map (one thread per tile, binary search over seg_tile256)
@@ -1215,7 +1226,8 @@ bool launch_pp(const AssignParams& p, const int32_t* tile_seg, const int32_t* se
 bool launch_pp_shape(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles,
                      int64_t cap, hipStream_t st) {
   constexpr int R = 256;
-  hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, R, seg_tiles);
+  hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, R,
+                     (int64_t)(cap / R + p.n_segments), p.work_count ? p.work_count + kErrSlot : (int32_t*)nullptr, seg_tiles);
   const int64_t max_tiles = cap / R + p.n_segments;
   const unsigned tg = (unsigned)(max_tiles / 256 + 1 < 4096 ? max_tiles / 256 + 1 : 4096);
   hipLaunchKernelGGL(tile_seg_kernel, dim3(tg), dim3(256), 0, st, seg_tiles, p.n_segments, cap, tile_seg);
@@ -1241,7 +1253,8 @@ template <int W, int S>
 bool launch_shape(const AssignParams& p, int nt, bool t3, int rl, bool norm, int32_t* tile_seg, int32_t* seg_tiles,
                   int64_t cap, hipStream_t st) {
   constexpr int R = W * 32;
-  hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, R, seg_tiles);
+  hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, R,
+                     (int64_t)(cap / R + p.n_segments), p.work_count ? p.work_count + kErrSlot : (int32_t*)nullptr, seg_tiles);
   const int64_t max_tiles = cap / R + p.n_segments;  // bound on the R-row tiles
   const unsigned tg = (unsigned)(max_tiles / 256 + 1 < 4096 ? max_tiles / 256 + 1 : 4096);
   hipLaunchKernelGGL(tile_seg_kernel, dim3(tg), dim3(256), 0, st, seg_tiles, p.n_segments, cap, tile_seg);
@@ -1273,7 +1286,8 @@ bool stream_supported(int nt, bool t3, int rl, bool norm) {
 }
 
 void launch_tiling(const AssignParams& p, int R, int32_t* tile_seg, int32_t* seg_tiles, int64_t cap, hipStream_t st) {
-  hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, R, seg_tiles);
+  hipLaunchKernelGGL(stream_tiles_kernel, dim3(1), dim3(1024), 0, st, p.seg_row_off, p.n_segments, R,
+                     (int64_t)(cap / R + p.n_segments), p.work_count ? p.work_count + kErrSlot : (int32_t*)nullptr, seg_tiles);
   const int64_t max_tiles = cap / R + p.n_segments;
   const unsigned tg = (unsigned)(max_tiles / 256 + 1 < 4096 ? max_tiles / 256 + 1 : 4096);
   hipLaunchKernelGGL(tile_seg_kernel, dim3(tg), dim3(256), 0, st, seg_tiles, p.n_segments, cap, tile_seg);

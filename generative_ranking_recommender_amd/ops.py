@@ -222,9 +222,10 @@ class AssignWorkspace:
         return int(self.buf[:4].view(torch.int32).item())
 
     def error(self) -> int:
-        """Sticky error word of every assign on this workspace (host sync; csrc/assign.hip kErrSlot):
-        bit 0 compaction past n_rows, bit 1 overflow list past n_rows, bit 2 a list entry outside work[].
-        Every such write is bounded by its slot's capacity; a non-zero word means one was dropped."""
+        """Sticky error word of every assign on this workspace (host sync; csrc/assign_common.h kErrSlot):
+        bit 0 compaction past n_rows, bit 1 overflow list past n_rows, bit 2 a list entry outside work[],
+        bit 3 a tile count past the tile maps / descriptors (clamped). Every such write or count is bounded by
+        its slot's capacity; a non-zero word means one was dropped."""
         return int(self.error_word().item())
 
     def error_word(self) -> torch.Tensor:
@@ -240,7 +241,7 @@ def check_error_words(words, what: str) -> None:
     vals = torch.cat(ws).cpu().tolist()
     if any(vals):
         raise RuntimeError(f"{what}: a device error word is set ({vals}): a counter-driven list write fell outside "
-                           "its slot and was dropped (csrc/assign.hip kErrSlot, rqsid_bucket)")
+                           "its slot and was dropped (csrc/assign_common.h kErrSlot, rqsid_bucket)")
 
 
 @dataclass

@@ -120,7 +120,9 @@ int32_t rqsid_assign_tile_rows(void);
  * Workspace bytes [240, 244) are a sticky error word the caller zeroes when it allocates the workspace
  * (every call zeroes only [0, 240)): each list write whose index comes from a device counter (the
  * re-score compaction, the overflow list) is bounded by its slot's capacity, and a write that would fall
- * outside sets a bit here instead (1 compaction, 2 overflow list, 4 a list entry outside [0, n_rows)). */
+ * outside sets a bit here instead (1 compaction, 2 overflow list, 4 a list entry outside [0, n_rows),
+ * 8 a device tile count past the tile maps / descriptors of the streamed, producer/consumer, row- and
+ * centre-resident screens: clamped to their capacity). */
 int64_t rqsid_assign_workspace_bytes(int64_t n_rows);
 int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row_index,
                  int32_t n_segments, const int32_t* seg_row_off, const int32_t* seg_tile_off,

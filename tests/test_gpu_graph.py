@@ -53,7 +53,7 @@ def test_encode_step_graph_replays_equal_eager():
 
 def test_encode_list_writes_stay_in_bounds():
     """Every write of the captured encode step whose index comes from a device counter -- rqsid_assign's
-    sentinel compaction and the fp32 re-screen's overflow list (csrc/assign.hip kErrSlot), rqsid_bucket's
+    sentinel compaction and the fp32 re-screen's overflow list (csrc/assign_common.h kErrSlot), rqsid_bucket's
     row_index scatter (csrc/rqsid.hip bucket_put) -- is bounded by its slot and raises a bit of a sticky error
     word instead of writing past it.  PROD codebooks, every level, eager and three back-to-back graph
     replays: every word stays 0 (the encoder's assign workspace and both of its bucket workspaces)."""
