@@ -25,6 +25,16 @@
 
 #include "internal.h"
 
+// diagnostic build only (-DRQSID_STAMPS, tools/auction_stamps.py): s_memtime cycles of the list round's phases
+// (thread 0 of every block that completes a list round) and of resolve blocks
+#ifdef RQSID_STAMPS
+__device__ unsigned long long g_al_stamps[16];
+#define AST(...) __VA_ARGS__
+#define ANOW() __builtin_amdgcn_s_memtime()
+#else
+#define AST(...)
+#endif
+
 namespace rqsid {
 namespace {
 
@@ -134,6 +144,10 @@ struct SegAuction {
   unsigned long long* rdone;
   uint32_t* js;                  // (list rounds) per job {winner & 0xFFFF, cost bits}: one gather per listed job
   int32_t rcount;                // end-of-round: add the live count for the host's poll (a block's last round)
+  // one-segment single-process auctions: the segment's job count (0 otherwise).  The segment, its chunks and its
+  // list layout are then arithmetic (segment 0, jobs [0, one_n), list capacity 4 * (one_n / K) + 256 at offset
+  // 0): the round kernels take them without the dependent table loads that open every block otherwise
+  int64_t one_n;
 };
 constexpr int64_t kListMaxJpw = 16384;  // one-block list rounds only while the average jobs per worker per segment is at most this
 constexpr int64_t kListBlockJpw = 8192;  // one wide segment above this many jobs per worker: multi-block list rounds
@@ -172,6 +186,15 @@ struct ChunkInfo {
 
 __device__ __forceinline__ ChunkInfo chunk_info(const SegAuction& a, int64_t c) {
   ChunkInfo ci;
+  if (a.one_n) {
+    ci.s = 0;
+    ci.seg_j0 = 0;
+    ci.n_s = a.one_n;
+    ci.cis = c;
+    ci.j0 = c * kCh;
+    ci.nj = min((int64_t)kCh, a.one_n - ci.j0);
+    return ci;
+  }
   ci.s = seg_of(a.chunk_off, a.S, c);
   ci.seg_j0 = a.seg_off[ci.s];
   ci.n_s = a.seg_off[ci.s + 1] - ci.seg_j0;
@@ -1326,22 +1349,50 @@ constexpr int kListEq = 2048;  // values equal to T a list round ranks in LDS (m
 constexpr int kLT = 1024;  // threads of a list-round block
 // LT threads per block: 1024, or 256 when every list is short (the middle layer's lockstep sub-fits: 128
 // segments x 128 workers, lists of ~500 entries, 16384 blocks per round)
+// Lists of at most kLE * LT entries stay in registers from the first load (entry tid + q * LT in er[q]): the
+// later passes read no list memory, and the first load is issued before the block's validity checks.
+constexpr int kLE = 4;
 template <int LT>
 __global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
   const int64_t hw = blockIdx.x;
   const int r = (int)(hw / a.K), w = (int)(hw % a.K);
-  const int sg = a.mseg[r];
+  const bool one = a.one_n > 0;  // (then n_multi == 1: r == 0, segment 0)
+  const int sg = one ? 0 : a.mseg[r];
+  const uint32_t cap = one ? (uint32_t)(4 * (a.one_n / a.K) + 256) : (uint32_t)a.lcs[r];
+  uint2* const L = a.lst + (one ? 0 : a.loff[r]) + (int64_t)w * cap;
+  const int tid = threadIdx.x;
+  const bool regs = cap <= (uint32_t)(kLE * LT);
+  uint2 er[kLE];
+  if (regs) {
+#pragma unroll
+    for (int q = 0; q < kLE; ++q) {
+      const uint32_t i = tid + q * LT;
+      er[q] = i < cap ? L[i] : make_uint2(0u, 0u);  // (in the worker's list area whatever n is)
+    }
+  }
   if (!(a.flag[sg] & kLive)) return;
   __shared__ uint32_t hst[256];
   __shared__ uint32_t sh[4];  // bin, above, T, need | radix-select bin and rank
-  const int tid = threadIdx.x;
   const int counter = *a.round_dev;
-  const uint32_t cap = (uint32_t)a.lcs[r];
   const uint32_t n = a.lcnt[hw * kAbovePad];
   const uint32_t kb = a.lkb[hw];
   const int64_t sw = (int64_t)sg * a.K + w;
-  const uint32_t jpw = (uint32_t)((a.seg_off[sg + 1] - a.seg_off[sg]) / a.K);
-  uint2* const L = a.lst + a.loff[r] + (int64_t)w * cap;
+  const uint32_t jpw = (uint32_t)((one ? a.one_n : (int64_t)(a.seg_off[sg + 1] - a.seg_off[sg])) / a.K);
+  // every list entry i < n with its 64-bit word, from registers or from the list
+  auto visit = [&](auto&& f) __attribute__((always_inline)) {
+    if (regs) {
+#pragma unroll
+      for (int q = 0; q < kLE; ++q) {
+        const uint32_t i = tid + q * LT;
+        if (i < n) f(er[q], i);
+      }
+    } else {
+      for (uint32_t i = tid; i < n; i += LT) {
+        uint2 e = L[i];
+        f(e, i);
+      }
+    }
+  };
   auto fail_list = [&]() {
     if (tid == 0) {
       a.lbad[hw] = 1;
@@ -1354,16 +1405,19 @@ __global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
     if (tid == 0) list_stat(a, list_fail_why(n, cap, counter));
     return fail_list();
   }
+  AST(const uint64_t s0 = ANOW(); uint64_t s1 = 0, s2 = 0, s3 = 0;)
   if (tid < 256) hst[tid] = 0;
   __syncthreads();
   // pass 1: this round's value keys (raw score, cost, last winner), kept in the entries' upper 16 bits so
   // the later passes read the list only
-  for (uint32_t i = tid; i < n; i += LT) {
-    const uint2 e = L[i];
-    const uint32_t k = okey(value_bits(w, (uint16_t)e.y, js_hb(a, e.x), js_cost(a, e.x)));
-    L[i].y = (e.y & 0xFFFFu) | (k << 16);
+  visit([&](uint2& e, uint32_t i) {
+    const int32_t hbj = js_hb(a, e.x);
+    const uint32_t k = okey(value_bits(w, (uint16_t)e.y, hbj, js_cost(a, e.x)));
+    e.y = (e.y & 0xFFFFu) | (k << 16);
+    if (!regs) L[i].y = e.y;
+    else if (hbj == w) e.x |= 0x80000000u;  // (register copy only: the retention test of the bid pass)
     if (k >= kb) atomicAdd(&hst[k >> 8], 1u);
-  }
+  });
   __syncthreads();
   if (tid < 64) {
     uint32_t tot = hst[4 * tid] + hst[4 * tid + 1] + hst[4 * tid + 2] + hst[4 * tid + 3];
@@ -1377,6 +1431,7 @@ __global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
   }
   __syncthreads();
   const uint32_t b1 = sh[0];
+  AST(s1 = ANOW();)
   if (b1 == 0xFFFFFFFFu) {  // fewer than jpw + 1 values at or above the list base
     if (tid == 0) list_stat(a, 5);
     return fail_list();
@@ -1384,10 +1439,10 @@ __global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
   __syncthreads();
   if (tid < 256) hst[tid] = 0;
   __syncthreads();
-  for (uint32_t i = tid; i < n; i += LT) {
-    const uint32_t k = L[i].y >> 16;
+  visit([&](uint2& e, uint32_t) {
+    const uint32_t k = e.y >> 16;
     if (k >= kb && (k >> 8) == b1) atomicAdd(&hst[k & 255u], 1u);
-  }
+  });
   __syncthreads();
   if (tid < 64) {
     uint32_t b = 0, above = 0;
@@ -1401,6 +1456,7 @@ __global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
   }
   __syncthreads();
   const uint32_t T = sh[2], need = sh[3];
+  AST(s2 = ANOW();)
   if (T < kb) return fail_list();  // (cannot happen with >= jpw + 1 values >= kb; kept as a guard)
   // the first `need` of the values equal to T in job order bid: J = the need-th smallest job index among
   // them, by a radix select over the index bytes (no sort, no bound on the number of equal values: fp16
@@ -1412,11 +1468,11 @@ __global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
       __syncthreads();
       if (tid < 256) hst[tid] = 0;
       __syncthreads();
-      for (uint32_t i = tid; i < n; i += LT) {
-        const uint2 e = L[i];
-        if ((e.y >> 16) == T && (shift == 24 || (e.x >> (shift + 8)) == J))
-          atomicAdd(&hst[(e.x >> shift) & 255u], 1u);
-      }
+      visit([&](uint2& e, uint32_t) {
+        const uint32_t j = e.x & 0x7FFFFFFFu;
+        if ((e.y >> 16) == T && (shift == 24 || (j >> (shift + 8)) == J))
+          atomicAdd(&hst[(j >> shift) & 255u], 1u);
+      });
       __syncthreads();
       if (tid < 64) {  // ascending walk: the bin holding the rank-th smallest
         const uint32_t h0 = hst[4 * tid], h1 = hst[4 * tid + 1], h2 = hst[4 * tid + 2], h3 = hst[4 * tid + 3];
@@ -1445,13 +1501,13 @@ __global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
       rank = sh[1];
     }
   }
+  AST(s3 = ANOW();)
   const uint16_t eps = a.eps[sg];
   const _Float16 epsh = __builtin_bit_cast(_Float16, eps);
   const _Float16 vT = __builtin_bit_cast(_Float16, okey_inv(T));
   const bool ret = counter < 100;
-  for (uint32_t i = tid; i < n; i += LT) {
-    const uint2 e = L[i];
-    const uint32_t j = e.x, k = e.y >> 16;
+  visit([&](uint2& e, uint32_t) {
+    const uint32_t j = e.x & 0x7FFFFFFFu, k = e.y >> 16;
     uint32_t bid = 0;
     if (k > T) {
       const _Float16 x = __builtin_bit_cast(_Float16, okey_inv(k));
@@ -1459,9 +1515,10 @@ __global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
     } else if (k == T && need && j <= J) {
       bid = eps;
     }
-    if (ret && js_hb(a, j) == w) bid = eps;  // retention: the previous winner bids eps on its job
+    if (ret && (regs ? (e.x >> 31) != 0u : js_hb(a, j) == w)) bid = eps;  // retention: the previous winner bids eps
     if (bid) atomicMax(&a.key[j], (bid << 16) | (0xFFFFu - (uint32_t)w));
-  }
+  });
+  AST(__syncthreads();)
   if (tid == 0) {
     uint32_t* sel = a.sel + sw * 4;
     sel[0] = T >> 8;
@@ -1470,6 +1527,16 @@ __global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
     sel[3] = need;
     a.lbad[hw] = 0;
     list_stat(a, 0);
+#ifdef RQSID_STAMPS
+    const uint64_t s4 = ANOW();
+    atomicAdd(&g_al_stamps[0], (unsigned long long)(s1 - s0));
+    atomicAdd(&g_al_stamps[1], (unsigned long long)(s2 - s1));
+    atomicAdd(&g_al_stamps[2], (unsigned long long)(s3 - s2));
+    atomicAdd(&g_al_stamps[3], (unsigned long long)(s4 - s3));
+    atomicAdd(&g_al_stamps[4], 1ull);
+    atomicAdd(&g_al_stamps[5], need ? 1ull : 0ull);
+    atomicAdd(&g_al_stamps[6], (unsigned long long)n);
+#endif
   }
 }
 
@@ -1694,7 +1761,14 @@ __global__ __launch_bounds__(256) void sa_resolve_kernel(SegAuction a, int32_t* 
   if (a.dmode && a.dmode[0] == 2) return;  // a void row-sharded slot changes no job state (kDVoid)
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
   if (!(a.flag[ci.s] & kLive)) return;
+  AST(const uint64_t r0 = ANOW();)
   resolve_chunk(a, ci, out);
+#ifdef RQSID_STAMPS
+  if (threadIdx.x == 0) {
+    atomicAdd(&g_al_stamps[8], (unsigned long long)(ANOW() - r0));
+    atomicAdd(&g_al_stamps[9], 1ull);
+  }
+#endif
 }
 
 // end of a round: a segment whose every job has a bidder is done (it was live from round 0, so its
@@ -1922,6 +1996,8 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
                     const int32_t* seg_chunk_off, int64_t total_chunks, int32_t n_multi, int64_t n_jobs,
                     const uint8_t* active, int32_t max_rounds, int32_t* out_assign, int32_t* out_rounds,
                     void* workspace, int64_t workspace_bytes, void* stream, bool vec) {
+  // (vec is passed only by rqsid_auction_lap_half, whose one segment it lays out itself: seg_off = {0, n_jobs})
+  const bool single_layout = vec && n_seg == 1;
   vec = vec && n_seg == 1 && n_jobs % 4 == 0 && ((uintptr_t)scores & 7) == 0;
   if (!scores || !seg_off || !seg_chunk_off || !out_assign || !out_rounds || n_workers <= 0 || n_seg <= 0 ||
       total_chunks < 0 || total_chunks > INT32_MAX || n_jobs < 0 || n_jobs > INT32_MAX || n_multi < 0 ||
@@ -1942,6 +2018,7 @@ int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, co
   a.chunk_off = seg_chunk_off;
   a.rounds = out_rounds;
   a.n_multi = n_multi;
+  a.one_n = single_layout && n_multi == 1 ? n_jobs : 0;
   Carve c{(char*)workspace};
   carve(a, c, n_jobs, n_workers, n_seg, total_chunks, true);
   const unsigned gs = (unsigned)cdiv(n_seg, 256);
@@ -2756,3 +2833,11 @@ int rqsid_dauction_list_pass(const uint16_t* scores, int32_t n_workers, int64_t 
 }
 
 }  // extern "C"
+
+#ifdef RQSID_STAMPS
+extern "C" int rqsid_debug_al_stamps(unsigned long long* out16) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_al_stamps), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  unsigned long long z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_al_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
