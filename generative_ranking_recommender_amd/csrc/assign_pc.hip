@@ -169,7 +169,18 @@ __global__ __launch_bounds__(768, 3) void assign_pc_kernel(AssignParams p, const
       }
     };
     // epilogue of tile T (its {m2, A2} were written by the producers in the phase before)
+    PST(uint64_t s_eM = 0, s_eU = 0, s_eB = 0, s_eD = 0;)
     auto epilogue = [&](const PcDesc& D, int par) __attribute__((always_inline)) {
+#ifdef RQSID_STAMPS
+      uint64_t e0 = PNOW();
+      {
+        float dmy;  // the last MFMA's result: the matrix pipe drained
+        asm volatile("v_mov_b32 %0, %1" : "=v"(dmy) : "v"(acc[NT - 1][15]));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(dmy));
+      }
+      s_eM += PNOW() - e0;
+      e0 = PNOW();
+#endif
       const unsigned char* hb = smem + L::kH + par * L::kHBytes;
       const int lr = 32 * c + r;
       const bool row_valid = lr < D.nrows;
@@ -219,6 +230,7 @@ __global__ __launch_bounds__(768, 3) void assign_pc_kernel(AssignParams p, const
         }
         U = fminf(U, xor32(U));
         const float Up = fmaf(fabsf(U), 0x1p-22f, U) + (1.2e-38f + 2e-30f);
+        PST(asm volatile("" ::"v"(Up)); s_eU += PNOW() - e0; e0 = PNOW();)
         const f2 upv = {Up, Up};
         uint32_t pbt[NT];
 #pragma unroll
@@ -250,6 +262,7 @@ __global__ __launch_bounds__(768, 3) void assign_pc_kernel(AssignParams p, const
             pbits[wd] &= m;
           }
         }
+        PST(asm volatile("" ::"v"(pbits[0]), "v"(pbits[NT / 2 - 1])); s_eB += PNOW() - e0; e0 = PNOW();)
         int k = -1;
         if (pass_decide(pbits, h, k, w)) {
           out_l = k;
@@ -264,6 +277,7 @@ __global__ __launch_bounds__(768, 3) void assign_pc_kernel(AssignParams p, const
         if (need) p.work[my_row] = w;
         if (RL == 1 && NORM) p.den_out[my_row] = reinterpret_cast<const float*>(smem + L::kCoef + lr * 16)[2];
       }
+      PST(s_eD += PNOW() - e0;)
     };
     lgkm_barrier();  // prologue barriers a, b, c (loaders: header, centres; producers: rows, B(0))
     lgkm_barrier();
@@ -303,6 +317,10 @@ __global__ __launch_bounds__(768, 3) void assign_pc_kernel(AssignParams p, const
       atomicAdd(&g_pc_stamps[3], (unsigned long long)s_epi);
       atomicAdd(&g_pc_stamps[4], 1ull);
       atomicAdd(&g_pc_stamps[5], (unsigned long long)s_cmp);
+      atomicAdd(&g_pc_stamps[2], (unsigned long long)s_eM);
+      atomicAdd(&g_pc_stamps[6], (unsigned long long)s_eU);
+      atomicAdd(&g_pc_stamps[7], (unsigned long long)s_eB);
+      atomicAdd(&g_pc_stamps[23], (unsigned long long)s_eD);
     }
 #endif
     return;

@@ -53,7 +53,8 @@ def main(n=int(os.environ.get("SWEEP_ROWS", 10_000_000))):
     encmod.ops.assign = orig
     wide = os.environ.get("PCW", "0") == "1"
     rows_t, ph_t, ncons = (256, 32, 8) if wide else (128, 16, 4)
-    names = {0: ("consumer", {1: "barrier", 5: "compute", 3: "epilogue"}),
+    names = {0: ("consumer", {1: "barrier", 5: "compute", 3: "epilogue", 2: "  epi:mfma-drain", 6: "  epi:bound+U",
+                              7: "  epi:pass-bits", 23: "  epi:decide+stores"}),
              8: ("producer", {6: "issue", 2: "vmcnt", 5: "build", 3: "finish", 1: "barrier"}),
              16: ("loader", {6: "issue", 2: "vmcnt", 1: "barrier"})}
     if wide:
