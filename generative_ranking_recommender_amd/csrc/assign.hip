@@ -1602,7 +1602,7 @@ int rqsid_assign(const float* x, int64_t n_rows, int32_t dim, const int32_t* row
   // 3-term <= 128 candidates, and level 2, 1-term <= 256); RQSID_PC=0 keeps the older
   // dispatch above for A/B, variant 9 forces it wherever it applies
   const char* pce = getenv("RQSID_PC");
-  const bool pc_ok = pc_supported(dim, cand_count_max, t3, res_levels) && !cand_lid &&
+  const bool pc_ok = pc_supported(dim, cand_count_max, t3, res_levels) &&
                      (res_levels != 1 || !norm || den_out) && (int64_t)n_segments + 1 <= n_rows &&
                      pc_desc_bytes(n_rows, n_segments) <= resident_desc_bytes(n_rows);
   // (default: the 1-term levels; RQSID_PC=2 takes the 3-term ones too, RQSID_PC=0 none)

@@ -265,7 +265,7 @@ __global__ __launch_bounds__(768, 3) void assign_pc_kernel(AssignParams p, const
         PST(asm volatile("" ::"v"(pbits[0]), "v"(pbits[NT / 2 - 1])); s_eB += PNOW() - e0; e0 = PNOW();)
         int k = -1;
         if (pass_decide(pbits, h, k, w)) {
-          out_l = k;
+          out_l = p.cand_lid ? cand_local(p, D.cbase, k) : k;  // (a deduplicated list reports the original local id)
           out_g = cand_of(k);
         } else {
           need = true;
@@ -817,7 +817,7 @@ __global__ __launch_bounds__(768, 3) void assign_pcw_kernel(AssignParams p, cons
         }
         int k = -1;
         if (pass_decide(pbits, h, k, w)) {
-          out_l = k;
+          out_l = p.cand_lid ? cand_local(p, D.cbase, k) : k;  // (a deduplicated list reports the original local id)
           out_g = !p.cand_idx ? D.cbase + min(k, D.cnt - 1) : reinterpret_cast<const int*>(hb + L::kHCidx)[min(k, 255)];
         } else {
           need = true;

@@ -459,6 +459,33 @@ def test_stream_kernel_equals_tile_kernel(shape, sem_name, form):
     assert (a[sel] == ref).all()
 
 
+@pytest.mark.parametrize("form", ["default", "pc128", "pcw"])
+def test_pc_screen_with_duplicate_centres(form):
+    """Deduplicated candidate lists (ops.dedup_candidates: bitwise-identical centres of one list keep the first,
+    the kept entries report their original local ids through cand_lid) through the producer/consumer screens:
+    duplicated children inside level-1 parent blocks and duplicated level-2 centres.  IDs equal the per-tile
+    screen's on every row and the exact oracle's on a sample (the reference's argmin takes the first equal
+    centre, which is what the local ids must report)."""
+    need, cb = (128, 128, 256), dict(synth.encode_codebooks(seed=99))
+    c1, c2 = cb["c1"].copy(), cb["c2"].copy()
+    for par in range(0, 128, 3):  # child 2 := child 9, child 40 := child 41 in every third parent
+        c1[par * 128 + 2] = c1[par * 128 + 9]
+        c1[par * 128 + 40] = c1[par * 128 + 41]
+    c2[1:2560:5] = c2[0:2560:5]
+    cb["c1"], cb["c2"] = c1, c2
+    xn = synth.mixture_rows(7, 40000)
+    x = gpu(xn)
+    enc = RQEncoder([torch.from_numpy(cb[k]) for k in ("c0", "c1", "c2")], list(need),
+                    match=torch.from_numpy(cb["match"]), semantics=HIERARCHICAL_TRAIN, device=DEV)
+    assert all(c is not None and c.lid is not None for c in enc.cands[1:]), "the lists were not deduplicated"
+    a = _with_env(STREAMED[form], lambda: enc.encode(x).cpu().numpy())
+    b = _with_env(PER_TILE, lambda: enc.encode(x).cpu().numpy())
+    assert (a == b).all(), f"{int((a != b).any(1).sum())} rows differ between the {form} and per-tile screens"
+    sel = np.arange(0, 40000, 41)
+    ref = O.encode(xn[sel], [cb["c0"], c1, c2], list(need), cb["match"], residual_from_weighted=True, exact=True)
+    assert (a[sel] == ref).all()
+
+
 @pytest.mark.parametrize("form", ["default", "s83", "pp88", "res", "rows443", "rows883"])
 @pytest.mark.parametrize("k", [100, 128, 200, 256])
 def test_stream_nearest_partial_tiles(k, form):
