@@ -1061,7 +1061,11 @@ __global__ __launch_bounds__(256) void sa_eqcount_kernel(SegAuction a) {
 // ---- resolve one chunk: winners, costs and the count of jobs with a bidder; every load issued before any
 // store.  (A bid kernel whose last block per chunk resolved it measured 17x slower: the cross-block
 // handoff needs device-scope fences, an L2 writeback per block on the XCD-split L2.) ----
-__device__ __forceinline__ void resolve_chunk(const SegAuction& a, const ChunkInfo& ci, int32_t* __restrict__ out) {
+// (live: the segment's flag, loaded by the caller and tested here, after the chunk's loads are issued)
+__device__ __forceinline__ void resolve_chunk(const SegAuction& a, const ChunkInfo& ci, int32_t* __restrict__ out,
+                                              const uint8_t* live = nullptr) {
+  const uint8_t fl = live ? *live : kLive;
+  const int counter = a.lst ? *a.round_dev : 0;
   uint32_t k[kJPT];
   uint16_t c[kJPT];
 #pragma unroll
@@ -1070,8 +1074,8 @@ __device__ __forceinline__ void resolve_chunk(const SegAuction& a, const ChunkIn
     k[t] = a.key[j];
     c[t] = a.cost[j];
   }
+  if (!(fl & kLive)) return;
   if (a.lst) {  // list mode: the retention / leftover bids of pairs no list held (the sweep's overrides)
-    const int counter = *a.round_dev;
     const uint32_t ek = (uint32_t)a.eps[ci.s] << 16;
     if (counter < 100 || counter > 1000) {
 #pragma unroll
@@ -1362,6 +1366,13 @@ __global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
   uint2* const L = a.lst + (one ? 0 : a.loff[r]) + (int64_t)w * cap;
   const int tid = threadIdx.x;
   const bool regs = cap <= (uint32_t)(kLE * LT);
+  // the block's state words and (register lists) the entries, all issued before any test: one round trip
+  const int64_t sw = (int64_t)sg * a.K + w;
+  const uint8_t sflag = a.flag[sg];
+  const int counter = *a.round_dev;
+  const uint32_t n = a.lcnt[hw * kAbovePad];
+  const uint32_t kb = a.lkb[hw];
+  const uint32_t tprev = a.sel[sw * 4 + 2];
   uint2 er[kLE];
   if (regs) {
 #pragma unroll
@@ -1370,13 +1381,9 @@ __global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
       er[q] = i < cap ? L[i] : make_uint2(0u, 0u);  // (in the worker's list area whatever n is)
     }
   }
-  if (!(a.flag[sg] & kLive)) return;
+  if (!(sflag & kLive)) return;
   __shared__ uint32_t hst[256];
   __shared__ uint32_t sh[4];  // bin, above, T, need | radix-select bin and rank
-  const int counter = *a.round_dev;
-  const uint32_t n = a.lcnt[hw * kAbovePad];
-  const uint32_t kb = a.lkb[hw];
-  const int64_t sw = (int64_t)sg * a.K + w;
   const uint32_t jpw = (uint32_t)((one ? a.one_n : (int64_t)(a.seg_off[sg + 1] - a.seg_off[sg])) / a.K);
   // every list entry i < n with its 64-bit word, from registers or from the list
   auto visit = [&](auto&& f) __attribute__((always_inline)) {
@@ -1401,7 +1408,7 @@ __global__ __launch_bounds__(LT) void sa_list_round_kernel(SegAuction a) {
       a.lcnt[hw * kAbovePad] = 0;  // the sweep's guessed pass rebuilds it
     }
   };
-  if (n == 0 || n > cap || counter > 1000 || a.sel[sw * 4 + 2] < kb) {
+  if (n == 0 || n > cap || counter > 1000 || tprev < kb) {
     if (tid == 0) list_stat(a, list_fail_why(n, cap, counter));
     return fail_list();
   }
@@ -1760,9 +1767,8 @@ __global__ void sa_list_layout_kernel(SegAuction a) {
 __global__ __launch_bounds__(256) void sa_resolve_kernel(SegAuction a, int32_t* __restrict__ out) {
   if (a.dmode && a.dmode[0] == 2) return;  // a void row-sharded slot changes no job state (kDVoid)
   const ChunkInfo ci = chunk_info(a, blockIdx.x);
-  if (!(a.flag[ci.s] & kLive)) return;
   AST(const uint64_t r0 = ANOW();)
-  resolve_chunk(a, ci, out);
+  resolve_chunk(a, ci, out, a.flag + ci.s);  // (the segment's flag tested after the chunk's loads are issued)
 #ifdef RQSID_STAMPS
   if (threadIdx.x == 0) {
     atomicAdd(&g_al_stamps[8], (unsigned long long)(ANOW() - r0));
