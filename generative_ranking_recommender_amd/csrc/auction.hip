@@ -315,7 +315,7 @@ int rqsid_auction_lap_half(const uint16_t* scores_wj, int32_t n_workers, int64_t
   if (rc) return rc;
   rc = seg_auction_run(scores_wj, n_workers, 1, seg_off, chunk_off, nch, nch > 1 ? 1 : 0, n_jobs, nullptr,
                        max_rounds, out_assign, rounds_dev, p + 3 * kSmallAlign, workspace_bytes - 3 * kSmallAlign,
-                       stream, true);
+                       stream, true, /*single_layout=*/true);
   if (rc) return rc;
   int32_t r = 0;
   if (hipMemcpyAsync(&r, rounds_dev, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||

@@ -2001,9 +2001,8 @@ namespace rqsid {
 int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, const int32_t* seg_off,
                     const int32_t* seg_chunk_off, int64_t total_chunks, int32_t n_multi, int64_t n_jobs,
                     const uint8_t* active, int32_t max_rounds, int32_t* out_assign, int32_t* out_rounds,
-                    void* workspace, int64_t workspace_bytes, void* stream, bool vec) {
-  // (vec is passed only by rqsid_auction_lap_half, whose one segment it lays out itself: seg_off = {0, n_jobs})
-  const bool single_layout = vec && n_seg == 1;
+                    void* workspace, int64_t workspace_bytes, void* stream, bool vec, bool single_layout) {
+  single_layout = single_layout && n_seg == 1;
   vec = vec && n_seg == 1 && n_jobs % 4 == 0 && ((uintptr_t)scores & 7) == 0;
   if (!scores || !seg_off || !seg_chunk_off || !out_assign || !out_rounds || n_workers <= 0 || n_seg <= 0 ||
       total_chunks < 0 || total_chunks > INT32_MAX || n_jobs < 0 || n_jobs > INT32_MAX || n_multi < 0 ||

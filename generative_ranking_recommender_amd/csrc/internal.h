@@ -34,11 +34,13 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // rqsid_seg_auction_lap_half with a switch for the 8-byte-load sweeps (auction_seg.hip); vec is honoured
-// only for one segment of N % 4 == 0 jobs with an 8-byte aligned score matrix
+// only for one segment of N % 4 == 0 jobs with an 8-byte aligned score matrix.  single_layout: the caller laid
+// the one segment out itself (seg_off = {0, n_jobs}, chunk_off = {0, chunks}: rqsid_auction_lap_half), so the
+// round kernels may take that geometry without reading the tables (SegAuction::one_n)
 int seg_auction_run(const uint16_t* scores, int32_t n_workers, int32_t n_seg, const int32_t* seg_off,
                     const int32_t* seg_chunk_off, int64_t total_chunks, int32_t n_multi, int64_t n_jobs,
                     const uint8_t* active, int32_t max_rounds, int32_t* out_assign, int32_t* out_rounds,
-                    void* workspace, int64_t workspace_bytes, void* stream, bool vec);
+                    void* workspace, int64_t workspace_bytes, void* stream, bool vec, bool single_layout = false);
 
 // exclusive-scan kernel shared by bucketing and the match-list builder (rqsid.hip)
 __global__ __launch_bounds__(1024) void bucket_scan_kernel(const int32_t* __restrict__ counts, int S, int tile_rows,
