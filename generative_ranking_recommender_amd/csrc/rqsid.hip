@@ -146,11 +146,12 @@ __device__ __forceinline__ void bucket_put(int32_t pos, unsigned k, int64_t i, c
 __global__ __launch_bounds__(256) void bucket_scatter_kernel(const int32_t* __restrict__ keys, int64_t n,
                                                              int S, int32_t* __restrict__ cursor,
                                                              const int32_t* __restrict__ row_off,
-                                                             int32_t* __restrict__ row_index, int32_t* __restrict__ err) {
+                                                             int32_t* __restrict__ row_index, int32_t* __restrict__ err,
+                                                             int64_t rows_per_block) {
   extern __shared__ __attribute__((aligned(16))) int32_t lh[];
   if (S <= kBucketLdsBins) {
-    const int64_t r0 = (int64_t)blockIdx.x * kScatterRowsPerBlock;
-    const int64_t r1 = r0 + kScatterRowsPerBlock < n ? r0 + kScatterRowsPerBlock : n;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
     for (int b = threadIdx.x; b < S; b += blockDim.x) lh[b] = 0;
     __syncthreads();
     for (int64_t i = r0 + threadIdx.x; i < r1; i += blockDim.x) {
@@ -631,8 +632,15 @@ int rqsid_bucket(const int32_t* keys, int64_t n, int32_t S, int32_t tile_rows, i
   int32_t* cursor = counts + S;
   if (fill_async(counts, 0, (size_t)S * 4, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "bucket: memset");
   const size_t lds = S <= kBucketLdsBins ? (size_t)S * 4 : 0;
+  // rows per LDS-histogram block: every block zeroes its S bins and adds each non-zero bin to the global count
+  // (hist) or reserves a cursor range for it (scatter), so many keys take bigger blocks (RQSID_BUCKET_WIDE: the
+  // rows per block for S > 4096, A/B)
+  const char* ebw = getenv("RQSID_BUCKET_WIDE");
+  const int64_t wide_rows = ebw ? std::max<int64_t>(4096, atoll(ebw)) : 32768;
+  const bool wide = S > 4096;
+  const int64_t hist_rows = wide ? wide_rows : 256 * 16, scat_rows = wide ? wide_rows : kScatterRowsPerBlock;
   if (n > 0) {
-    hipLaunchKernelGGL(bucket_hist_kernel, dim3(grid_cap(cdiv(n, 256 * 16), 2048)), dim3(256), lds, st, keys, n,
+    hipLaunchKernelGGL(bucket_hist_kernel, dim3(grid_cap(cdiv(n, hist_rows), 2048)), dim3(256), lds, st, keys, n,
                        S, counts);
     if ((rc = check_launch("bucket_hist"))) return rc;
   }
@@ -640,10 +648,9 @@ int rqsid_bucket(const int32_t* keys, int64_t n, int32_t S, int32_t tile_rows, i
                      seg_tile_off, cursor);
   if ((rc = check_launch("bucket_scan"))) return rc;
   if (n > 0) {
-    const unsigned blocks = S <= kBucketLdsBins ? (unsigned)cdiv(n, kScatterRowsPerBlock)
-                                                : grid_cap(cdiv(n, 256 * 16), 2048);
+    const unsigned blocks = S <= kBucketLdsBins ? (unsigned)cdiv(n, scat_rows) : grid_cap(cdiv(n, 256 * 16), 2048);
     hipLaunchKernelGGL(bucket_scatter_kernel, dim3(blocks), dim3(256), lds, st, keys, n, S, cursor, seg_row_off,
-                       row_index, cursor + S);
+                       row_index, cursor + S, (int64_t)scat_rows);
     if ((rc = check_launch("bucket_scatter"))) return rc;
   }
   return RQSID_OK;
