@@ -99,6 +99,25 @@ def test_seg_auction_small_groups_against_oracle(levels):
         assert np.array_equal(a[lay.off[s]:lay.off[s + 1]], np.asarray(want, dtype=np.int64)), s
 
 
+def test_seg_auction_repeat_calls_with_rewritten_scores():
+    """Repeated auctions over one score buffer rewritten in place between calls (the K-Means iterations' pattern):
+    the round blocks instantiated by one call are replayed by the next when the buffers and shapes agree, so
+    each call must still read the new scores (every result against the oracle)."""
+    k = 8
+    sizes = np.array([67, 2100, 130], dtype=np.int64)
+    flat = torch.empty(int(sizes.sum()) * k, dtype=torch.float16, device=DEV)
+    lay = ops.SegmentLayout(sizes, DEV)
+    for it in range(3):
+        rng = np.random.default_rng(100 + it)
+        blocks = [_random_scores(rng, k, int(n), 7 + 500 * it) for n in sizes]
+        flat.copy_(torch.from_numpy(np.concatenate([b.reshape(-1) for b in blocks])))
+        a, _ = ops.seg_auction(flat, k, lay)
+        a = a.cpu().numpy()
+        for s in range(len(sizes)):
+            want = O.auction_lap_half(blocks[s].T.astype(np.float32), tie_rule="stable")
+            assert np.array_equal(a[lay.off[s]:lay.off[s + 1]], np.asarray(want, dtype=np.int64)), (it, s)
+
+
 def _segments(sizes, seed):
     x = synth.small_mixture(int(np.sum(sizes)), m=24, seed=seed)
     return torch.from_numpy(x).to(DEV), ops.SegmentLayout(np.asarray(sizes, dtype=np.int64), DEV)
