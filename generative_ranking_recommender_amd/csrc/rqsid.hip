@@ -87,47 +87,46 @@ __global__ __launch_bounds__(256) void bucket_hist_kernel(const int32_t* __restr
   }
 }
 
-// One block: exclusive scans of counts and ceil(counts / tile_rows).
+// One block: exclusive scans of counts and ceil(counts / tile_rows).  Thread t owns the contiguous run of
+// ceil(S / 1024) keys starting at t * run: it sums its run, the block scans the 1024 run sums, and the thread
+// writes its run's offsets (one pass of the block scan instead of one per 1024 keys: 160 -> ~5 us at S = 65536).
 __global__ __launch_bounds__(1024) void bucket_scan_kernel(const int32_t* __restrict__ counts, int S,
                                                            int tile_rows, int32_t* __restrict__ row_off,
                                                            int32_t* __restrict__ tile_off,
                                                            int32_t* __restrict__ cursor) {
   __shared__ int32_t sa[1024], sb[1024];
-  __shared__ int32_t carry[2];
   const int t = threadIdx.x;
-  if (t == 0) carry[0] = carry[1] = 0;
+  const int run = (S + 1023) / 1024;
+  const int k0 = t * run < S ? t * run : S, k1 = k0 + run < S ? k0 + run : S;
+  int32_t a = 0, b = 0;
+  for (int k = k0; k < k1; ++k) {
+    const int32_t c = counts[k];
+    a += c;
+    b += tile_rows > 0 ? (c + tile_rows - 1) / tile_rows : 0;
+  }
+  sa[t] = a;
+  sb[t] = b;
   __syncthreads();
-  for (int base = 0; base < S; base += 1024) {
-    const int i = base + t;
-    const int32_t a = i < S ? counts[i] : 0;
-    const int32_t b = tile_rows > 0 ? (a + tile_rows - 1) / tile_rows : 0;
-    sa[t] = a;
-    sb[t] = b;
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int32_t va = t >= o ? sa[t - o] : 0;
+    const int32_t vb = t >= o ? sb[t - o] : 0;
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-      const int32_t va = t >= o ? sa[t - o] : 0;
-      const int32_t vb = t >= o ? sb[t - o] : 0;
-      __syncthreads();
-      sa[t] += va;
-      sb[t] += vb;
-      __syncthreads();
-    }
-    const int32_t ea = carry[0] + sa[t] - a, eb = carry[1] + sb[t] - b;
-    if (i < S) {
-      row_off[i] = ea;
-      if (tile_off) tile_off[i] = eb;
-      if (cursor) cursor[i] = ea;
-    }
-    __syncthreads();
-    if (t == 1023) {
-      carry[0] += sa[1023];
-      carry[1] += sb[1023];
-    }
+    sa[t] += va;
+    sb[t] += vb;
     __syncthreads();
   }
-  if (t == 0) {
-    row_off[S] = carry[0];
-    if (tile_off) tile_off[S] = carry[1];
+  int32_t ea = sa[t] - a, eb = sb[t] - b;
+  for (int k = k0; k < k1; ++k) {
+    const int32_t c = counts[k];
+    row_off[k] = ea;
+    if (tile_off) tile_off[k] = eb;
+    if (cursor) cursor[k] = ea;
+    ea += c;
+    eb += tile_rows > 0 ? (c + tile_rows - 1) / tile_rows : 0;
+  }
+  if (t == 1023) {
+    row_off[S] = sa[1023];
+    if (tile_off) tile_off[S] = sb[1023];
   }
 }
 
@@ -175,6 +174,159 @@ __global__ __launch_bounds__(256) void bucket_scatter_kernel(const int32_t* __re
       const unsigned k = (unsigned)keys[i];
       if (k >= (unsigned)S) continue;
       bucket_put(atomicAdd(&cursor[k], 1), k, i, row_off, row_index, err);
+    }
+  }
+}
+
+// Many keys (4096 < S <= 262144): a count matrix instead of device-wide atomics.  The rows split into B chunks
+// (B x S <= 4M words, B <= 256) and the keys into slices of kBucketLdsBins; block (b, s) counts chunk b's keys
+// of slice s in LDS and stores them as row b of the matrix (no atomics outside LDS), a column scan turns each
+// column into the chunks' exclusive prefixes and the key's total (and sums each 64 keys), the offsets kernel
+// scans the totals (each 64-key block adds the sums of the blocks before it: no one-block serial scan), and the
+// scatter block (b, s) starts each key of its slice at row_off[k] + prefix[b][k].  The global-atomic form
+// (S > 16384) cost 235 + 277 us at 6.25M rows over 65536 keys (the XL last level), plus 160 us of one-block
+// scan; the LDS-histogram form flushes ~S global atomics per block.  Blocks of one chunk share an XCD (B is a
+// multiple of 8) and so its keys; 1024 threads with kBucketUnroll keys in flight each hide the load latency of
+// the few blocks (B x slices).
+constexpr int64_t kBucketMatrixWords = int64_t(1) << 22;
+constexpr int kBucketUnroll = 8;
+// chunks of the count matrix for S keys (its workspace is sized for every S <= 262144; `min_keys` is the
+// smallest S that takes it)
+inline int bucket_chunks(int64_t n, int S, int min_keys = 1) {
+  if (S < min_keys || S > 262144 || n <= 0) return 0;
+  return (int)std::min<int64_t>(256, kBucketMatrixWords / S) / 8 * 8;
+}
+
+__global__ __launch_bounds__(1024) void bucket_chunk_hist_kernel(const int32_t* __restrict__ keys, int64_t n, int S,
+                                                                 int64_t chunk_rows, int32_t* __restrict__ mat) {
+  extern __shared__ __attribute__((aligned(16))) int32_t lh[];
+  const int b0 = blockIdx.y * kBucketLdsBins;
+  const int nb = S - b0 < kBucketLdsBins ? S - b0 : kBucketLdsBins;
+  for (int j = threadIdx.x; j < nb; j += blockDim.x) lh[j] = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * chunk_rows;
+  const int64_t r1 = r0 + chunk_rows < n ? r0 + chunk_rows : n;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += (int64_t)blockDim.x * kBucketUnroll) {
+    unsigned d[kBucketUnroll];
+#pragma unroll
+    for (int u = 0; u < kBucketUnroll; ++u) {
+      const int64_t r = i + (int64_t)u * blockDim.x;
+      d[u] = r < r1 ? (unsigned)keys[r] - (unsigned)b0 : ~0u;  // keys outside [0, S) fall outside every slice
+    }
+#pragma unroll
+    for (int u = 0; u < kBucketUnroll; ++u)
+      if (d[u] < (unsigned)nb) atomicAdd(&lh[d[u]], 1);
+  }
+  __syncthreads();
+  int32_t* row = mat + (int64_t)blockIdx.x * S + b0;
+  for (int j = threadIdx.x; j < nb; j += blockDim.x) row[j] = lh[j];
+}
+
+__device__ __forceinline__ int32_t bucket_wave_sum(int32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ int32_t bucket_wave_incl_scan(int32_t v, int lane) {
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// Column scan of the [B][S] count matrix: a block takes 64 keys, its 4 waves a quarter of the chunks each (held
+// in registers), so the loads of a column are all in flight at once.  counts[k] = the key's total; bsum[blk],
+// bsum[nblk + blk] = the block's row and tile totals.
+constexpr int kBucketMaxChunks = 256;
+__global__ __launch_bounds__(256) void bucket_chunk_scan_kernel(int32_t* __restrict__ mat, int B, int S, int tile_rows,
+                                                                int32_t* __restrict__ counts, int32_t* __restrict__ bsum) {
+  __shared__ int32_t qs[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  const int q = (B + 3) / 4, c0 = w * q;
+  int32_t v[kBucketMaxChunks / 4];
+  int32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < kBucketMaxChunks / 4; ++j) {
+    v[j] = 0;
+    if (j < q && c0 + j < B && k < S) v[j] = mat[(int64_t)(c0 + j) * S + k];
+    sum += v[j];
+  }
+  qs[w][lane] = sum;
+  __syncthreads();
+  int32_t run = 0;
+  for (int u = 0; u < w; ++u) run += qs[u][lane];
+  if (k < S) {
+#pragma unroll
+    for (int j = 0; j < kBucketMaxChunks / 4; ++j) {
+      if (j < q && c0 + j < B) mat[(int64_t)(c0 + j) * S + k] = run;
+      run += v[j];
+    }
+    if (w == 3) counts[k] = run;
+  }
+  if (w == 3) {
+    const int32_t c = k < S ? run : 0;
+    const int32_t a = bucket_wave_sum(c);
+    const int32_t t = bucket_wave_sum(tile_rows > 0 ? (c + tile_rows - 1) / tile_rows : 0);
+    if (lane == 0) {
+      bsum[blockIdx.x] = a;
+      bsum[gridDim.x + blockIdx.x] = t;
+    }
+  }
+}
+
+// row_off / tile_off from the key totals: one wave per 64 keys, offset = the sums of the blocks before it.
+__global__ __launch_bounds__(64) void bucket_chunk_offsets_kernel(const int32_t* __restrict__ counts,
+                                                                  const int32_t* __restrict__ bsum, int S,
+                                                                  int tile_rows, int32_t* __restrict__ row_off,
+                                                                  int32_t* __restrict__ tile_off) {
+  const int lane = threadIdx.x, blk = blockIdx.x, nblk = gridDim.x;
+  int32_t a = 0, t = 0;
+  for (int j = lane; j < blk; j += 64) {
+    a += bsum[j];
+    t += bsum[nblk + j];
+  }
+  a = bucket_wave_sum(a);
+  t = bucket_wave_sum(t);
+  const int k = blk * 64 + lane;
+  const int32_t c = k < S ? counts[k] : 0;
+  const int32_t tc = tile_rows > 0 ? (c + tile_rows - 1) / tile_rows : 0;
+  const int32_t ia = bucket_wave_incl_scan(c, lane), it = bucket_wave_incl_scan(tc, lane);
+  if (k < S) {
+    row_off[k] = a + ia - c;
+    if (tile_off) tile_off[k] = t + it - tc;
+  }
+  if (blk == nblk - 1 && lane == 63) {
+    row_off[S] = a + ia;
+    if (tile_off) tile_off[S] = t + it;
+  }
+}
+
+__global__ __launch_bounds__(1024) void bucket_chunk_scatter_kernel(const int32_t* __restrict__ keys, int64_t n, int S,
+                                                                    int64_t chunk_rows, const int32_t* __restrict__ mat,
+                                                                    const int32_t* __restrict__ row_off,
+                                                                    int32_t* __restrict__ row_index,
+                                                                    int32_t* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) int32_t lh[];
+  const int b0 = blockIdx.y * kBucketLdsBins;
+  const int nb = S - b0 < kBucketLdsBins ? S - b0 : kBucketLdsBins;
+  const int32_t* row = mat + (int64_t)blockIdx.x * S + b0;
+  for (int j = threadIdx.x; j < nb; j += blockDim.x) lh[j] = row_off[b0 + j] + row[j];
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * chunk_rows;
+  const int64_t r1 = r0 + chunk_rows < n ? r0 + chunk_rows : n;
+  for (int64_t i = r0 + threadIdx.x; i < r1; i += (int64_t)blockDim.x * kBucketUnroll) {
+    unsigned k[kBucketUnroll];
+#pragma unroll
+    for (int u = 0; u < kBucketUnroll; ++u) {
+      const int64_t r = i + (int64_t)u * blockDim.x;
+      k[u] = r < r1 ? (unsigned)keys[r] : ~0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kBucketUnroll; ++u) {
+      const unsigned d = k[u] - (unsigned)b0;
+      if (d < (unsigned)nb)
+        bucket_put(atomicAdd(&lh[d], 1), k[u], i + (int64_t)u * blockDim.x, row_off, row_index, err);
     }
   }
 }
@@ -570,6 +722,12 @@ int ensure_attrs() {
   e = hipFuncSetAttribute((const void*)bucket_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                           kBucketLdsBins * 4);
   if (e != hipSuccess) return fail(RQSID_E_LAUNCH, "set smem attr (scatter): %s", hipGetErrorString(e));
+  e = hipFuncSetAttribute((const void*)bucket_chunk_hist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          kBucketLdsBins * 4);
+  if (e != hipSuccess) return fail(RQSID_E_LAUNCH, "set smem attr (chunk hist): %s", hipGetErrorString(e));
+  e = hipFuncSetAttribute((const void*)bucket_chunk_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          kBucketLdsBins * 4);
+  if (e != hipSuccess) return fail(RQSID_E_LAUNCH, "set smem attr (chunk scatter): %s", hipGetErrorString(e));
   g_attr_done[dev] = true;
   return RQSID_OK;
 }
@@ -612,10 +770,12 @@ const char* rqsid_last_error(void) { return g_err; }
 int32_t rqsid_centroid_tile_rows(void) { return kAccTileRows; }
 
 // workspace: counts i32[S] | cursor i32[S] | 64 ints: [0] the sticky error word (zeroed by the caller when it
-// allocates the workspace, never by a call: include/rqsid.h)
+// allocates the workspace, never by a call: include/rqsid.h) | for 4096 < S <= 262144 the [B][S] count matrix
+// (B x S <= 4M words: 16 MiB, independent of n so that one workspace serves every call with these keys)
 int64_t rqsid_bucket_workspace_bytes(int64_t n, int32_t n_segments) {
   (void)n;
-  return ((int64_t)n_segments * 2 + 64) * 4;
+  const int64_t B = bucket_chunks(1, n_segments);
+  return ((int64_t)n_segments * 2 + 64 + (B ? B * n_segments + 2 * cdiv(n_segments, 64) : 0)) * 4;
 }
 
 int rqsid_bucket(const int32_t* keys, int64_t n, int32_t S, int32_t tile_rows, int32_t* seg_row_off,
@@ -630,6 +790,25 @@ int rqsid_bucket(const int32_t* keys, int64_t n, int32_t S, int32_t tile_rows, i
   hipStream_t st = (hipStream_t)stream;
   int32_t* counts = (int32_t*)workspace;
   int32_t* cursor = counts + S;
+  // RQSID_BUCKET_MATRIX (A/B): 0 the LDS-histogram / global-atomic forms for every S, 2 the count matrix for every S
+  const char* ebm = getenv("RQSID_BUCKET_MATRIX");
+  const int bm = ebm ? atoi(ebm) : 1;
+  const int B = bm == 0 ? 0 : bucket_chunks(n, S, bm == 2 ? 1 : 4097);
+  if (B > 0) {
+    int32_t* mat = cursor + S + 64;
+    int32_t* bsum = mat + (int64_t)B * S;
+    const int64_t chunk_rows = cdiv(n, B);
+    const dim3 grid((unsigned)B, (unsigned)cdiv(S, kBucketLdsBins));
+    const size_t lds = (size_t)kBucketLdsBins * 4;
+    const unsigned nblk = (unsigned)cdiv(S, 64);
+    hipLaunchKernelGGL(bucket_chunk_hist_kernel, grid, dim3(1024), lds, st, keys, n, S, chunk_rows, mat);
+    hipLaunchKernelGGL(bucket_chunk_scan_kernel, dim3(nblk), dim3(256), 0, st, mat, B, S, tile_rows, counts, bsum);
+    hipLaunchKernelGGL(bucket_chunk_offsets_kernel, dim3(nblk), dim3(64), 0, st, counts, bsum, S, tile_rows,
+                       seg_row_off, seg_tile_off);
+    hipLaunchKernelGGL(bucket_chunk_scatter_kernel, grid, dim3(1024), lds, st, keys, n, S, chunk_rows, mat,
+                       seg_row_off, row_index, cursor + S);
+    return check_launch("bucket_chunk");
+  }
   if (fill_async(counts, 0, (size_t)S * 4, st) != hipSuccess) return fail(RQSID_E_LAUNCH, "bucket: memset");
   const size_t lds = S <= kBucketLdsBins ? (size_t)S * 4 : 0;
   // rows per LDS-histogram block: every block zeroes its S bins and adds each non-zero bin to the global count

@@ -159,19 +159,27 @@ def test_residual_golden(golden):
     assert np.array_equal(got[:256], g["res_plain_head"])
 
 
-def test_bucket_is_grouped_permutation():
-    keys = np.random.default_rng(1).integers(0, 300, 100000).astype(np.int32)
-    keys[:5000] = 7  # one big segment
-    b = ops.bucket(gpu(keys), 300)
+# key counts of every bucketing form (csrc/rqsid.hip rqsid_bucket): LDS histograms (300, and 8192 with the count
+# matrix off), the count matrix with one slice (8192, 16384; forced for 300 and 128), several and a ragged last slice (65536, 70001), and
+# device-wide atomics (65536 with the matrix off); row counts below the matrix's chunk count and empty
+@pytest.mark.parametrize("S,n,matrix", [(300, 100000, 1), (300, 100000, 2), (128, 3000, 2), (8192, 100000, 1), (8192, 100000, 0), (16384, 300000, 1),
+                                        (65536, 1000000, 1), (65536, 1000000, 0), (70001, 500000, 1), (65536, 50, 1),
+                                        (65536, 0, 1)])
+def test_bucket_is_grouped_permutation(S, n, matrix, monkeypatch):
+    monkeypatch.setenv("RQSID_BUCKET_MATRIX", str(matrix))
+    keys = np.random.default_rng(S + n).integers(0, S, n).astype(np.int32)
+    keys[:n // 20] = 7  # one big segment
+    ws = ops.bucket_workspace(S, DEV)
+    b = ops.bucket(gpu(keys), S, workspace=ws)
     off = b.seg_row_off.cpu().numpy()
     idx = b.row_index.cpu().numpy()
     assert off[0] == 0 and off[-1] == len(keys)
-    assert np.array_equal(np.diff(off), np.bincount(keys, minlength=300))
+    assert np.array_equal(np.diff(off), np.bincount(keys, minlength=S))
     assert np.array_equal(np.sort(idx), np.arange(len(keys)))
-    for s in (0, 7, 299):
-        assert (keys[idx[off[s]:off[s + 1]]] == s).all()
+    assert (keys[idx] == np.repeat(np.arange(S), np.diff(off))).all()
     toff = b.seg_tile_off.cpu().numpy()
     assert np.array_equal(np.diff(toff), (np.diff(off) + 127) // 128)
+    assert int(ops.bucket_error_word(ws, S).item()) == 0
 
 
 def test_segmented_assign_with_match_lists():

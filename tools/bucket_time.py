@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
-"""Time rqsid_bucket (ops.bucket) on 10M uniform keys at S = 128 and 16384 (HIP events, 10 calls) and check the
-result is a counting sort (keys non-decreasing along row_index, every row once).  RQSID_BUCKET_WIDE sets the
-rows per block for S > 4096 (A/B)."""
+"""Time rqsid_bucket (ops.bucket) on N uniform keys (default 10M at S = 128 and 16384, the PROD levels; BUCKET_N
+and BUCKET_S="256,65536" for the XL ones) with HIP events over 10 calls, and check the result is a counting sort
+(keys non-decreasing along row_index, every row once).  RQSID_BUCKET_WIDE sets the rows per block for S > 4096
+(A/B)."""
 import os, sys, time, torch
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
 from generative_ranking_recommender_amd import ops
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(3)
-for S in (128, 16384):
-    keys = torch.randint(0, S, (10_000_000,), device=dev, generator=g, dtype=torch.int32)
+N = int(os.environ.get("BUCKET_N", 10_000_000))
+for S in [int(v) for v in os.environ.get("BUCKET_S", "128,16384").split(",")]:
+    keys = torch.randint(0, S, (N,), device=dev, generator=g, dtype=torch.int32)
     ws = ops.bucket_workspace(S, dev)
     for _ in range(3):
         b = ops.bucket(keys, S, workspace=ws)
