@@ -159,10 +159,10 @@ def test_residual_golden(golden):
     assert np.array_equal(got[:256], g["res_plain_head"])
 
 
-# key counts of every bucketing form (csrc/rqsid.hip rqsid_bucket): LDS histograms (300, and 8192 with the count
-# matrix off), the count matrix with one slice (8192, 16384; forced for 300 and 128), several and a ragged last slice (65536, 70001), and
+# key counts of every bucketing form (csrc/rqsid.hip rqsid_bucket): LDS histograms (300 and 8192 with the count
+# matrix off), the count matrix with one slice (128, 300, 8192, 16384), several and a ragged last slice (65536, 70001), and
 # device-wide atomics (65536 with the matrix off); row counts below the matrix's chunk count and empty
-@pytest.mark.parametrize("S,n,matrix", [(300, 100000, 1), (300, 100000, 2), (128, 3000, 2), (8192, 100000, 1), (8192, 100000, 0), (16384, 300000, 1),
+@pytest.mark.parametrize("S,n,matrix", [(300, 100000, 1), (300, 100000, 0), (128, 3000, 1), (8192, 100000, 1), (8192, 100000, 0), (16384, 300000, 1),
                                         (65536, 1000000, 1), (65536, 1000000, 0), (70001, 500000, 1), (65536, 50, 1),
                                         (65536, 0, 1)])
 def test_bucket_is_grouped_permutation(S, n, matrix, monkeypatch):
