@@ -190,10 +190,16 @@ __global__ __launch_bounds__(256) void bucket_scatter_kernel(const int32_t* __re
 // the few blocks (B x slices).
 constexpr int64_t kBucketMatrixWords = int64_t(1) << 22;
 constexpr int kBucketUnroll = 8;
-// chunks of the count matrix for S keys (S <= 262144; more keys take the global-atomic form)
+// chunks of the count matrix for S keys (S <= 262144; more keys take the global-atomic form): at most
+// bucket_max_chunks(S) (the workspace's matrix), and ~32K rows per chunk for small inputs (at least 8 chunks), so
+// the column scan of a 100k-row call reads 8 rows of the matrix, not 256
+inline int bucket_max_chunks(int S) {
+  return S > 262144 ? 0 : (int)std::min<int64_t>(256, kBucketMatrixWords / S) / 8 * 8;
+}
 inline int bucket_chunks(int64_t n, int S) {
-  if (S > 262144 || n <= 0) return 0;
-  return (int)std::min<int64_t>(256, kBucketMatrixWords / S) / 8 * 8;
+  if (n <= 0) return 0;
+  const int64_t want = std::max<int64_t>(8, cdiv(n, 32768) / 8 * 8);
+  return (int)std::min<int64_t>(bucket_max_chunks(S), want);
 }
 
 __global__ __launch_bounds__(1024) void bucket_chunk_hist_kernel(const int32_t* __restrict__ keys, int64_t n, int S,
@@ -773,7 +779,7 @@ int32_t rqsid_centroid_tile_rows(void) { return kAccTileRows; }
 // (B x S <= 4M words: 16 MiB, independent of n so that one workspace serves every call with these keys)
 int64_t rqsid_bucket_workspace_bytes(int64_t n, int32_t n_segments) {
   (void)n;
-  const int64_t B = bucket_chunks(1, n_segments);
+  const int64_t B = bucket_max_chunks(n_segments);
   return ((int64_t)n_segments * 2 + 64 + (B ? B * n_segments + 2 * cdiv(n_segments, 64) : 0)) * 4;
 }
 
